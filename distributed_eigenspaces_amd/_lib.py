@@ -1,0 +1,105 @@
+"""ctypes binding of libdeig.so (the C ABI declared in include/deig.h).
+
+ctypes releases the GIL for the duration of each call, so several
+``my_threading.Slave`` worker threads can drive the GPU concurrently.
+There is no CPU fallback: if the library is missing the import of an op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdeig.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "deig.h")
+
+DEIG_OK = 0
+DEIG_NOT_CONVERGED = 1
+DEIG_EINVAL = -1
+DEIG_EHIP = -2
+DEIG_EWORKSPACE = -3
+
+_c_i64 = ctypes.c_int64
+_c_sz = ctypes.c_size_t
+_vp = ctypes.c_void_p
+_fp = ctypes.c_void_p  # device pointers are passed as integers
+
+SIGNATURES = {
+    "deig_version": (ctypes.c_int, []),
+    "deig_last_error": (ctypes.c_char_p, []),
+    "deig_syrk_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, ctypes.c_float, _fp, _c_i64,
+                                     _vp, _c_sz, _vp]),
+    "deig_syrk_workspace": (_c_sz, [_c_i64, _c_i64]),
+    "deig_default_subspace": (ctypes.c_int, [_c_i64, ctypes.c_int]),
+    "deig_topk_sym_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_float, _fp, ctypes.c_int, _c_i64,
+                                         _fp, _c_i64, _fp, ctypes.POINTER(ctypes.c_int),
+                                         ctypes.POINTER(ctypes.c_float), _vp, _c_sz, _vp]),
+    "deig_topk_workspace": (_c_sz, [_c_i64, ctypes.c_int, ctypes.c_int]),
+    "deig_projavg_topk_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, ctypes.c_float,
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_float, _fp, ctypes.c_int, _c_i64, _fp,
+                                             _c_i64, _fp, ctypes.POINTER(ctypes.c_int),
+                                             ctypes.POINTER(ctypes.c_float), _vp, _c_sz, _vp]),
+    "deig_projavg_workspace": (_c_sz, [_c_i64, _c_i64, ctypes.c_int, ctypes.c_int]),
+    "deig_oja_step_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, ctypes.c_float, _fp,
+                                         ctypes.c_int, _c_i64, _vp, _c_sz, _vp]),
+    "deig_oja_workspace": (_c_sz, [_c_i64, _c_i64, ctypes.c_int]),
+    "deig_project_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, _fp, ctypes.c_int, _c_i64,
+                                        _fp, _c_i64, _vp, _c_sz, _vp]),
+    "deig_project_workspace": (_c_sz, [_c_i64, _c_i64, ctypes.c_int]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class DeigError(RuntimeError):
+    """A libdeig call failed (HIP error or workspace problem)."""
+
+
+class NotConvergedWarning(RuntimeWarning):
+    """The eigensolver stopped at max_sweeps above its residual tolerance."""
+
+
+def header_symbols(path: str = HEADER):
+    """Function names declared in include/deig.h."""
+    txt = open(path).read()
+    return sorted(set(re.findall(r"\b(deig_[a-z0-9_]+)\s*\(", txt)))
+
+
+def lib() -> ctypes.CDLL:
+    """Load libdeig.so (once).  Raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"{LIB_PATH} is missing: build it with `python __graft_entry__.py build` "
+                    "(hipcc, gfx950).  There is no CPU fallback.")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    msg = lib().deig_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str) -> int:
+    """Map a libdeig return code to Python exceptions (0 and NOT_CONVERGED pass)."""
+    if rc in (DEIG_OK, DEIG_NOT_CONVERGED):
+        return rc
+    msg = f"{what}: {last_error()} (code {rc})"
+    if rc == DEIG_EINVAL:
+        raise ValueError(msg)
+    raise DeigError(msg)

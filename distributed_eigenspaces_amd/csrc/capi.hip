@@ -1,0 +1,263 @@
+// extern "C" boundary of libdeig.so (declared in include/deig.h) and the host
+// drivers of the two eigensolvers.  No device allocation happens here: all
+// device memory is caller-provided (PyTorch tensors on the Python side).
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "deig_internal.hpp"
+
+namespace deig {
+
+static thread_local char g_err[1024] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int num_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    (void)hipGetLastError();
+    return 256;  // MI355X; only reached by workspace queries without a device
+  }
+  if (!cache[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        v <= 0) {
+      (void)hipGetLastError();
+      v = 256;
+    }
+    cache[dev] = v;
+  }
+  return cache[dev];
+}
+
+namespace {
+
+constexpr int kMaxP = 128;
+
+struct Operator {
+  bool implicit;
+  const float* S;
+  int64_t lds;
+  const float* Wt;
+  int64_t mk, ldw;
+  float scale;
+};
+
+struct SolverWs {
+  RRBuffers rr;
+  float* Zt;
+  float* slab;
+  size_t slab_bytes;
+};
+
+SolverWs carve_solver(void* ws, size_t cap, int64_t d, int k, int p, int64_t mk, size_t* total) {
+  Carve c(ws, cap);
+  SolverWs w;
+  w.rr.Z = c.take<float>((size_t)d * 2 * p);
+  w.rr.C = c.take<float>((size_t)4 * p * p);
+  w.rr.Linv = c.take<float>((size_t)p * p);
+  w.rr.Wtmp = c.take<float>((size_t)p * p);
+  w.rr.W = c.take<float>((size_t)p * p);
+  w.rr.lam = c.take<float>((size_t)p);
+  w.rr.cs = c.take<float>((size_t)p);
+  w.rr.resid_part = c.take<float>((size_t)rr_update_blocks(d) * k);
+  w.rr.resid = c.take<float>((size_t)k + 1);
+  w.rr.info = c.take<int>(16);
+  w.Zt = mk > 0 ? c.take<float>((size_t)mk * p) : nullptr;
+  size_t sb = skinny_workspace_bytes(2 * p, 2 * p, d);  // Gram
+  if (mk > 0) {
+    const size_t a = skinny_workspace_bytes(mk, p, d);  // Wt Q
+    const size_t b = skinny_workspace_bytes(d, p, mk);  // Wt^T Zt
+    if (a > sb) sb = a;
+    if (b > sb) sb = b;
+  } else {
+    const size_t a = skinny_workspace_bytes(d, p, d);  // S Q
+    if (a > sb) sb = a;
+  }
+  w.slab = c.take<float>(sb / sizeof(float) + 4);
+  w.slab_bytes = sb;
+  *total = c.off;
+  return w;
+}
+
+int apply_op(const Operator& op, const SolverWs& w, int64_t d, int p, hipStream_t st) {
+  float* Q = w.rr.Z;
+  float* Y = w.rr.Z + p;
+  const int64_t ld = 2 * p;
+  if (!op.implicit)
+    return skinny_launch(true, op.S, op.lds, Q, ld, Y, ld, d, p, d, 1.f, 0.f, w.slab,
+                         w.slab_bytes, st);
+  int rc = skinny_launch(false, op.Wt, op.ldw, Q, ld, w.Zt, p, op.mk, p, d, 1.f, 0.f, w.slab,
+                         w.slab_bytes, st);
+  if (rc) return rc;
+  return skinny_launch(true, op.Wt, op.ldw, w.Zt, p, Y, ld, d, p, op.mk, op.scale, 0.f, w.slab,
+                       w.slab_bytes, st);
+}
+
+int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol, const float* Q0,
+          int k0, int64_t ldq0, float* V, int64_t ldv, float* evals, int* sweeps_out,
+          float* resid_out, void* ws, size_t ws_bytes, hipStream_t st) {
+  DEIG_REQUIRE(d >= 16 && d % 4 == 0, "solver: d=%lld must be >= 16 and a multiple of 4",
+               (long long)d);
+  DEIG_REQUIRE(k >= 1 && k <= d, "solver: need 1 <= k <= d (k=%d, d=%lld)", k, (long long)d);
+  if (p <= 0) p = deig_default_subspace(d, k);
+  DEIG_REQUIRE(p % 16 == 0 && p >= k && p <= kMaxP && p <= d,
+               "solver: subspace p=%d must be a multiple of 16 with k <= p <= min(128, d)", p);
+  DEIG_REQUIRE(max_sweeps >= 1, "solver: max_sweeps must be >= 1");
+  DEIG_REQUIRE(V && evals && ldv >= d, "solver: bad V / evals / ldv");
+  DEIG_REQUIRE(k0 >= 0 && k0 <= p && (k0 == 0 || (Q0 && ldq0 >= d)), "solver: bad warm start");
+  size_t total = 0;
+  SolverWs w = carve_solver(ws, ws_bytes, d, k, p, op.implicit ? op.mk : 0, &total);
+  if (!ws || total > ws_bytes)
+    return fail(DEIG_EWORKSPACE, "solver: workspace %zu bytes < required %zu", ws_bytes, total);
+
+  int rc = rr_init_launch(w.rr.Z, d, p, Q0, k0, ldq0, 0x5eed5eedull, st);
+  if (rc) return rc;
+  float best = 3.4e38f;
+  int since_best = 0;
+  int it = 0;
+  float last = 3.4e38f;
+  bool converged = false;
+  for (it = 0; it < max_sweeps; ++it) {
+    if ((rc = apply_op(op, w, d, p, st))) return rc;
+    if ((rc = skinny_launch(true, w.rr.Z, 2 * p, w.rr.Z, 2 * p, w.rr.C, 2 * p, 2 * p, 2 * p, d,
+                            1.f, 0.f, w.slab, w.slab_bytes, st)))
+      return rc;
+    if ((rc = rr_small_launch(w.rr, p, st))) return rc;
+    if ((rc = rr_update_launch(w.rr, d, p, k, V, ldv, evals, st))) return rc;
+    DEIG_HIP_CHECK(hipMemcpyAsync(&last, w.rr.resid + k, sizeof(float), hipMemcpyDeviceToHost, st));
+    DEIG_HIP_CHECK(hipStreamSynchronize(st));
+    if (!(last == last)) {  // NaN
+      if (sweeps_out) *sweeps_out = it + 1;
+      if (resid_out) *resid_out = last;
+      return fail(DEIG_EINVAL, "solver: non-finite residual (input contains NaN/Inf?)");
+    }
+    if (last <= tol) {
+      converged = true;
+      break;
+    }
+    // Stagnation at the fp32 floor: no 10% improvement for 4 sweeps.
+    if (last < 0.9f * best) {
+      best = last;
+      since_best = 0;
+    } else if (++since_best >= 4 && it >= 8) {
+      converged = true;
+      break;
+    }
+  }
+  if (sweeps_out) *sweeps_out = converged ? it + 1 : max_sweeps;
+  if (resid_out) *resid_out = last;
+  if (!converged)
+    return fail(DEIG_NOT_CONVERGED, "solver: residual %g > tol %g after %d sweeps", last, tol,
+                max_sweeps);
+  return DEIG_OK;
+}
+
+}  // namespace
+}  // namespace deig
+
+using namespace deig;
+
+extern "C" {
+
+int deig_version(void) { return 0x000100; }
+
+const char* deig_last_error(void) { return g_err; }
+
+size_t deig_syrk_workspace(int64_t n, int64_t d) { return syrk_workspace_bytes(n, d); }
+
+int deig_syrk_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha, float* S,
+                  int64_t lds, void* ws, size_t ws_bytes, void* stream) {
+  g_err[0] = 0;
+  return syrk_launch(X, n, d, ldx, alpha, S, lds, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int deig_default_subspace(int64_t d, int k) {
+  int64_t p = ((int64_t)k + (k < 16 ? 8 : k / 4) + 15) / 16 * 16;
+  if (p > kMaxP) p = kMaxP;
+  if (p > d) p = d / 16 * 16;
+  if (p < k) p = (k + 15) / 16 * 16;
+  return (int)p;
+}
+
+size_t deig_topk_workspace(int64_t d, int k, int p) {
+  if (p <= 0) p = deig_default_subspace(d, k);
+  size_t total = 0;
+  carve_solver(nullptr, 0, d, k, p, 0, &total);
+  return total;
+}
+
+int deig_topk_sym_f32(const float* S, int64_t d, int64_t lds, int k, int p, int max_sweeps,
+                      float tol, const float* Q0, int k0, int64_t ldq0, float* V, int64_t ldv,
+                      float* evals, int* sweeps_out, float* resid_out, void* ws, size_t ws_bytes,
+                      void* stream) {
+  g_err[0] = 0;
+  if (!S || lds < d || lds % 4 != 0 || !aligned16(S))
+    return fail(DEIG_EINVAL, "topk: S must be 16-byte aligned with lds >= d, lds %% 4 == 0");
+  Operator op{};
+  op.implicit = false;
+  op.S = S;
+  op.lds = lds;
+  return solve(op, d, k, p, max_sweeps, tol, Q0, k0, ldq0, V, ldv, evals, sweeps_out, resid_out,
+               ws, ws_bytes, (hipStream_t)stream);
+}
+
+size_t deig_projavg_workspace(int64_t d, int64_t mk, int k, int p) {
+  if (p <= 0) p = deig_default_subspace(d, k);
+  size_t total = 0;
+  carve_solver(nullptr, 0, d, k, p, mk, &total);
+  return total;
+}
+
+int deig_projavg_topk_f32(const float* Wt, int64_t d, int64_t mk, int64_t ldw, float scale, int k,
+                          int p, int max_sweeps, float tol, const float* Q0, int k0, int64_t ldq0,
+                          float* V, int64_t ldv, float* evals, int* sweeps_out, float* resid_out,
+                          void* ws, size_t ws_bytes, void* stream) {
+  g_err[0] = 0;
+  if (!Wt || mk < 1 || ldw < d || ldw % 4 != 0 || !aligned16(Wt))
+    return fail(DEIG_EINVAL, "projavg: Wt must be 16-byte aligned, mk >= 1, ldw >= d, ldw %% 4 == 0");
+  Operator op{};
+  op.implicit = true;
+  op.Wt = Wt;
+  op.mk = mk;
+  op.ldw = ldw;
+  op.scale = scale;
+  return solve(op, d, k, p, max_sweeps, tol, Q0, k0, ldq0, V, ldv, evals, sweeps_out, resid_out,
+               ws, ws_bytes, (hipStream_t)stream);
+}
+
+size_t deig_oja_workspace(int64_t b, int64_t d, int k) { return oja_workspace_bytes(b, d, k); }
+
+int deig_oja_step_f32(const float* Xb, int64_t b, int64_t d, int64_t ldx, float eta, float* V,
+                      int k, int64_t ldv, void* ws, size_t ws_bytes, void* stream) {
+  g_err[0] = 0;
+  if (!Xb || !V || !aligned16(Xb)) return fail(DEIG_EINVAL, "oja: Xb must be 16-byte aligned");
+  return oja_launch(Xb, b, d, ldx, eta, V, k, ldv, ws, ws_bytes, (hipStream_t)stream);
+}
+
+size_t deig_project_workspace(int64_t n, int64_t d, int k) {
+  return project_workspace_bytes(n, d, k);
+}
+
+int deig_project_f32(const float* X, int64_t n, int64_t d, int64_t ldx, const float* W, int k,
+                     int64_t ldw, float* Y, int64_t ldy, void* ws, size_t ws_bytes, void* stream) {
+  g_err[0] = 0;
+  return project_launch(X, n, d, ldx, W, k, ldw, Y, ldy, ws, ws_bytes, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,102 @@
+// Internal declarations shared by the libdeig translation units (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/deig.h"
+
+namespace deig {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+// ---------------------------------------------------------------- error handling
+void set_error(const char* fmt, ...);
+int fail(int code, const char* fmt, ...);
+
+#define DEIG_HIP_CHECK(expr)                                                          \
+  do {                                                                                \
+    hipError_t e__ = (expr);                                                          \
+    if (e__ != hipSuccess)                                                            \
+      return ::deig::fail(DEIG_EHIP, "%s:%d %s: %s", __FILE__, __LINE__, #expr,       \
+                          hipGetErrorString(e__));                                    \
+  } while (0)
+
+#define DEIG_REQUIRE(cond, ...)                                                       \
+  do {                                                                                \
+    if (!(cond)) return ::deig::fail(DEIG_EINVAL, __VA_ARGS__);                       \
+  } while (0)
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Number of CUs of the current device (cached per device id).
+int num_cus();
+
+// Workspace carving helper: hands out 256-byte aligned slices.
+struct Carve {
+  char* base;
+  size_t cap;
+  size_t off = 0;
+  Carve(void* b, size_t c) : base(static_cast<char*>(b)), cap(c) {}
+  template <class T>
+  T* take(size_t count) {
+    off = align_up(off, 256);
+    T* p = reinterpret_cast<T*>(base ? base + off : nullptr);
+    off += count * sizeof(T);
+    return p;
+  }
+  bool ok() const { return off <= cap; }
+};
+
+// ---------------------------------------------------------------- launchers
+// Covariance SYRK (syrk.hip).
+size_t syrk_workspace_bytes(int64_t n, int64_t d);
+int syrk_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha, float* S,
+                int64_t lds, void* ws, size_t ws_bytes, hipStream_t stream);
+
+// Skinny GEMM (skinny.hip):  C[M x N] = alpha * op(A) * B + beta * C
+//   trans_a = true : A is K x M row-major (op(A) = A^T)
+//   trans_a = false: A is M x K row-major
+//   B is K x N row-major; N % 16 == 0, N <= 256.
+size_t skinny_workspace_bytes(int64_t M, int64_t N, int64_t K);
+int skinny_launch(bool trans_a, const float* A, int64_t lda, const float* B, int64_t ldb,
+                  float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha,
+                  float beta, float* slab, size_t slab_bytes, hipStream_t stream);
+
+// Rayleigh-Ritz pieces (rr.hip).
+struct RRBuffers {
+  float* Z;          // d x 2p row-major: [Q | Y]
+  float* C;          // 2p x 2p Gram of Z
+  float* Linv;       // p x p
+  float* Wtmp;       // p x p
+  float* W;          // p x p, columns sorted by descending Ritz value
+  float* lam;        // p, descending
+  float* cs;         // p, column scales (0 = dead column)
+  float* resid_part; // nblk_update x k
+  float* resid;      // k  (relative residual per top-k column; [k] = max)
+  int* info;         // small int scratch
+};
+int rr_init_launch(float* Z, int64_t d, int p, const float* Q0, int k0, int64_t ldq0,
+                   uint64_t seed, hipStream_t stream);
+int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream);
+int rr_update_blocks(int64_t d);
+int rr_update_launch(const RRBuffers& b, int64_t d, int p, int k, float* V, int64_t ldv,
+                     float* evals, hipStream_t stream);
+
+// Oja (oja.hip).
+size_t oja_workspace_bytes(int64_t b, int64_t d, int k);
+int oja_launch(const float* Xb, int64_t b, int64_t d, int64_t ldx, float eta, float* V,
+               int k, int64_t ldv, void* ws, size_t ws_bytes, hipStream_t stream);
+
+// Projection Y = X W (project.hip).
+size_t project_workspace_bytes(int64_t n, int64_t d, int k);
+int project_launch(const float* X, int64_t n, int64_t d, int64_t ldx, const float* W, int k,
+                   int64_t ldw, float* Y, int64_t ldy, void* ws, size_t ws_bytes, hipStream_t st);
+
+}  // namespace deig

@@ -1,0 +1,153 @@
+// Mini-batch Oja step for the online / streaming variant (BASELINE.json config 4):
+//   V <- orth(V + eta/b * Xb^T (Xb V)),   orth = Cholesky-QR2.
+// Not present in the reference (parity unpinned; judged by sin(theta) against
+// the one-shot float64 oracle).  Xb is read twice (Xb V and Xb^T T), each pass a
+// skinny GEMM at ~k/2 flop/B (HBM-bound for k <= 32).
+#include "deig_internal.hpp"
+
+namespace deig {
+namespace {
+
+__global__ __launch_bounds__(256) void col_to_rowpad(const float* __restrict__ V, int64_t ldv,
+                                                     int64_t d, int k, int kp,
+                                                     float* __restrict__ Vr) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= d * kp) return;
+  const int64_t r = idx / kp;
+  const int j = (int)(idx - r * kp);
+  Vr[idx] = (j < k) ? V[r + (int64_t)j * ldv] : 0.f;
+}
+
+__global__ __launch_bounds__(256) void rowpad_to_col(const float* __restrict__ Vr, int64_t d,
+                                                     int k, int kp, float* __restrict__ V,
+                                                     int64_t ldv) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= d * k) return;
+  const int j = (int)(idx / d);
+  const int64_t r = idx - (int64_t)j * d;
+  V[r + (int64_t)j * ldv] = Vr[r * kp + j];
+}
+
+// G (kp x kp, leading k x k used) = L L^T;  Rinv = L^-T (upper), zero-padded to kp.
+__global__ __launch_bounds__(256) void chol_rinv_kernel(const float* __restrict__ G, int k, int kp,
+                                                        float* __restrict__ Rinv) {
+  __shared__ float L[64 * 64];
+  __shared__ float Li[64 * 64];
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < k * k; idx += 256) {
+    const int a = idx / k, b = idx - a * k;
+    L[idx] = G[a * kp + b];
+    Li[idx] = 0.f;
+  }
+  __syncthreads();
+  for (int j = 0; j < k; ++j) {
+    if (tid == 0) {
+      float v = L[j * k + j];
+      const float ref = fabsf(G[0]) > 0.f ? fabsf(G[0]) : 1.f;
+      if (!(v > 1e-12f * ref)) v = 1e-12f * ref;
+      L[j * k + j] = sqrtf(v);
+    }
+    __syncthreads();
+    const float inv = 1.0f / L[j * k + j];
+    for (int i = j + 1 + tid; i < k; i += 256) L[i * k + j] *= inv;
+    __syncthreads();
+    const int n = k - j - 1;
+    for (int idx = tid; idx < n * n; idx += 256) {
+      const int i = j + 1 + idx / n, c = j + 1 + idx % n;
+      if (c <= i) L[i * k + c] -= L[i * k + j] * L[c * k + j];
+    }
+    __syncthreads();
+  }
+  for (int i = 0; i < k; ++i) {
+    const float inv = 1.0f / L[i * k + i];
+    for (int c = tid; c <= i; c += 256) {
+      float s = (c == i) ? 1.0f : 0.0f;
+      for (int t = c; t < i; ++t) s -= L[i * k + t] * Li[t * k + c];
+      Li[i * k + c] = s * inv;
+    }
+    __syncthreads();
+  }
+  for (int idx = tid; idx < kp * kp; idx += 256) {
+    const int a = idx / kp, b = idx - a * kp;
+    Rinv[idx] = (a < k && b < k) ? Li[b * k + a] : 0.f;
+  }
+}
+
+struct OjaWs {
+  float *Vr, *Vr2, *T, *G, *Rinv, *slab;
+  size_t slab_bytes;
+};
+
+OjaWs carve_oja(void* ws, size_t cap, int64_t b, int64_t d, int kp, size_t* total) {
+  Carve c(ws, cap);
+  OjaWs o;
+  o.Vr = c.take<float>((size_t)d * kp);
+  o.Vr2 = c.take<float>((size_t)d * kp);
+  o.T = c.take<float>((size_t)b * kp);
+  o.G = c.take<float>((size_t)kp * kp);
+  o.Rinv = c.take<float>((size_t)kp * kp);
+  size_t sb = skinny_workspace_bytes(b, kp, d);
+  size_t s2 = skinny_workspace_bytes(d, kp, b);
+  size_t s3 = skinny_workspace_bytes(kp, kp, d);
+  size_t s4 = skinny_workspace_bytes(d, kp, kp);
+  if (s2 > sb) sb = s2;
+  if (s3 > sb) sb = s3;
+  if (s4 > sb) sb = s4;
+  o.slab = c.take<float>(sb / sizeof(float) + 1);
+  o.slab_bytes = sb;
+  *total = c.off;
+  return o;
+}
+
+}  // namespace
+
+size_t oja_workspace_bytes(int64_t b, int64_t d, int k) {
+  const int kp = (int)cdiv(k, 16) * 16;
+  size_t total = 0;
+  carve_oja(nullptr, 0, b, d, kp, &total);
+  return total;
+}
+
+int oja_launch(const float* Xb, int64_t b, int64_t d, int64_t ldx, float eta, float* V, int k,
+               int64_t ldv, void* ws, size_t ws_bytes, hipStream_t st) {
+  DEIG_REQUIRE(b >= 1 && d >= 4 && d % 4 == 0, "oja: need b >= 1 and d %% 4 == 0");
+  DEIG_REQUIRE(k >= 1 && k <= 64 && k <= d, "oja: need 1 <= k <= min(64, d)");
+  DEIG_REQUIRE(ldx >= d && ldx % 4 == 0 && ldv >= d, "oja: bad leading dims");
+  const int kp = (int)cdiv(k, 16) * 16;
+  size_t total = 0;
+  OjaWs o = carve_oja(ws, ws_bytes, b, d, kp, &total);
+  if (!ws || total > ws_bytes) return fail(DEIG_EWORKSPACE, "oja: workspace %zu < %zu", ws_bytes, total);
+  int rc;
+  hipLaunchKernelGGL(col_to_rowpad, dim3((unsigned)cdiv(d * kp, 256)), dim3(256), 0, st, V, ldv, d,
+                     k, kp, o.Vr);
+  DEIG_HIP_CHECK(hipGetLastError());
+  // T = Xb V
+  if ((rc = skinny_launch(false, Xb, ldx, o.Vr, kp, o.T, kp, b, kp, d, 1.f, 0.f, o.slab,
+                          o.slab_bytes, st)))
+    return rc;
+  // V += eta/b * Xb^T T
+  if ((rc = skinny_launch(true, Xb, ldx, o.T, kp, o.Vr, kp, d, kp, b, eta / (float)b, 1.f, o.slab,
+                          o.slab_bytes, st)))
+    return rc;
+  float* cur = o.Vr;
+  float* nxt = o.Vr2;
+  for (int pass = 0; pass < 2; ++pass) {
+    if ((rc = skinny_launch(true, cur, kp, cur, kp, o.G, kp, kp, kp, d, 1.f, 0.f, o.slab,
+                            o.slab_bytes, st)))
+      return rc;
+    hipLaunchKernelGGL(chol_rinv_kernel, dim3(1), dim3(256), 0, st, o.G, k, kp, o.Rinv);
+    DEIG_HIP_CHECK(hipGetLastError());
+    if ((rc = skinny_launch(false, cur, kp, o.Rinv, kp, nxt, kp, d, kp, kp, 1.f, 0.f, o.slab,
+                            o.slab_bytes, st)))
+      return rc;
+    float* t = cur;
+    cur = nxt;
+    nxt = t;
+  }
+  hipLaunchKernelGGL(rowpad_to_col, dim3((unsigned)cdiv(d * k, 256)), dim3(256), 0, st, cur, d, k,
+                     kp, V, ldv);
+  DEIG_HIP_CHECK(hipGetLastError());
+  return DEIG_OK;
+}
+
+}  // namespace deig

@@ -1,0 +1,245 @@
+"""Drop-in for the reference's ``distributed.py`` (TimeEscaper/distributed_eigenspaces).
+
+Same classes, methods, arguments, message schema and CLI flags; the arithmetic
+runs on the GPU through the HIP hot path:
+
+* ``SlaveNode.compute_sigma_hat_``  (distributed.py:59-70)  -> fp32-MFMA SYRK
+* ``Node.top_k_eigenvectors``       (distributed.py:22-29)  -> subspace iteration + RR
+* ``MasterNode.callback_`` average  (distributed.py:126-130) -> implicit projector-average
+  top-k (the reference builds the d x d sigma_tilde and discards it; the notebook's
+  server solve, raw line 306, is what is computed here - without forming d x d).
+
+Transport: the reference uses pika/RabbitMQ (out of scope).  ``broker_host`` names
+an in-process broker (``broker.py``) with the same channel API; requests and
+responses are the same JSON documents
+(request ``{"rank": k, "batch": [lo, hi]}``, response
+``{"batch": [lo, hi], "eigenspace": d x k nested list}``, distributed.py:49-52,
+:109-112).
+
+Deliberate differences (all additive; none changes a result for inputs the
+reference accepts):
+* the master's initial window is ``min(5, batches_number)`` instead of 5 (the
+  reference raises IndexError for batches_number < 5, distributed.py:108-111);
+* when the last shard arrives the master stores its result (``self.result``,
+  ``self.eigenspace``) and calls ``channel.stop_consuming()`` so ``start()`` returns;
+* ``top_k_eigenvectors`` / ``compute_sigma_hat_`` accept torch tensors on the GPU
+  and then return GPU tensors (numpy in -> numpy float64 out, like the reference).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import time
+
+import numpy as np
+import torch
+
+from . import broker as _broker
+from . import linalg
+
+__all__ = ["Node", "SlaveNode", "MasterNode", "run_master", "run_slave", "main",
+           "top_k_eigenvectors", "top_k_eigh", "compute_sigma_hat"]
+
+WINDOW = 5  # requests in flight at start (distributed.py:108)
+
+
+def _is_numpy(x) -> bool:
+    return isinstance(x, np.ndarray) or not isinstance(x, torch.Tensor)
+
+
+def top_k_eigh(matrix, k: int):
+    """(eigenvalues ascending, eigenvectors d x k ascending) of a symmetric matrix."""
+    res = linalg.topk_eigh(matrix, int(k))
+    if _is_numpy(matrix):
+        w = res.evals.double().cpu().numpy()
+        v = np.asfortranarray(res.V.double().cpu().numpy())
+        return w, v
+    return res.evals, res.V
+
+
+def top_k_eigenvectors(matrix, k: int):
+    """``Node.top_k_eigenvectors`` (distributed.py:22-29): top-k eigenvectors, ascending."""
+    return top_k_eigh(matrix, k)[1]
+
+
+def compute_sigma_hat(x):
+    """``SlaveNode.compute_sigma_hat_`` (distributed.py:59-70): X^T X / n, uncentered."""
+    S = linalg.sigma_hat(x)
+    if _is_numpy(x):
+        return S.double().cpu().numpy()
+    return S
+
+
+class Node:
+    """distributed.py:13-29: broker connection + top-k helper."""
+
+    def __init__(self, broker_host):
+        self.connection = _broker.connect(broker_host)
+        self.channel = self.connection.channel()
+        self.channel.queue_declare(queue="master")
+        self.channel.queue_declare(queue="slaves")
+
+    def top_k_eigenvectors(self, matrix, k):
+        return top_k_eigenvectors(matrix, k)
+
+
+class SlaveNode(Node):
+    """distributed.py:32-70: worker.  Keeps a device copy of ``data`` so each
+    request only slices it (the reference slices a host view, :46)."""
+
+    def __init__(self, broker_host, data):
+        super().__init__(broker_host)
+        print("Slave Start listening")
+        self.data = data
+        self._dev = None
+        self.channel.basic_consume(queue="slaves", on_message_callback=self.callback_)
+
+    def start(self):
+        self.channel.start_consuming()
+
+    def _device_data(self):
+        if self._dev is None:
+            self._dev = linalg.require_device_tensor(self.data, "SlaveNode.data")
+        return self._dev
+
+    def callback_(self, channel, method, properties, body):
+        request = json.loads(body)
+        print("Slave: Received, batchid: " + str(request["batch"]))
+        lo, hi = request["batch"][0], request["batch"][1]
+        batch = self._device_data()[lo:hi]
+        eigenspace = self.compute_sigma_hat_(batch)
+        eigenspace = self.top_k_eigenvectors(eigenspace, request["rank"])
+        response = dict()
+        response["batch"] = request["batch"]
+        response["eigenspace"] = eigenspace.double().cpu().numpy().tolist()
+        self.send_to_master_(str(json.dumps(response)))
+        channel.basic_ack(delivery_tag=method.delivery_tag)
+
+    def send_to_master_(self, message):
+        print("Sending to Master")
+        self.channel.basic_publish(exchange="", routing_key="master", body=message)
+
+    def compute_sigma_hat_(self, x):
+        return compute_sigma_hat(x)
+
+
+class MasterNode(Node):
+    """distributed.py:82-143: shard split, dispatch window, projector average."""
+
+    def __init__(self, broker_host, rank, batches_number, data):
+        super().__init__(broker_host)
+        self.rank = rank
+        self.batches_number = batches_number
+        self.data = data
+        self.batches_in_process = set()
+        self.batches = list()
+        self.computed_eigens = list()
+        self.current_batch = 0
+        self.result = None      # linalg.EigResult of the server solve
+        self.eigenspace = None  # numpy float64 d x k, ascending (NB:306 semantics)
+        self.eigenvalues = None
+        print("Master Start listening")
+        self.start_time = time.time()
+        self.channel.basic_consume(queue="master", on_message_callback=self.callback_)
+
+    def start(self):
+        print("Splitting dataset...")
+        step = self.data.shape[0] // self.batches_number
+        for i in range(self.batches_number):
+            batch = (i * step, (i + 1) * step)
+            self.batches.append(batch)
+            self.batches_in_process.add(batch)
+        print("Sending to slaves...")
+        for _ in range(min(WINDOW, len(self.batches))):
+            request = dict()
+            request["rank"] = self.rank
+            request["batch"] = self.batches.pop()
+            self.send_to_slaves_(str(json.dumps(request)))
+        print("Start waiting for messages")
+        self.channel.start_consuming()
+
+    def callback_(self, channel, method, properties, body):
+        request = json.loads(body)
+        batch = (request["batch"][0], request["batch"][1])
+        print("Master: Received, batch: " + str(batch))
+        eigenspace = np.array(request["eigenspace"])
+        self.computed_eigens.append(eigenspace)
+        self.batches_in_process.remove(batch)
+        if len(self.batches_in_process) == 0:
+            self.result = self.server_solve_()
+            self.eigenvalues = self.result.evals.double().cpu().numpy()
+            self.eigenspace = np.asfortranarray(self.result.V.double().cpu().numpy())
+            print("Computed! Time (seconds): " + str(time.time() - self.start_time))
+            channel.basic_ack(delivery_tag=method.delivery_tag)
+            self.channel.stop_consuming()
+            return
+        elif len(self.batches) != 0:
+            request = dict()
+            request["batch"] = self.batches.pop()
+            request["rank"] = self.rank
+            self.send_to_slaves_(str(json.dumps(request)))
+            print("Sended batch: " + str(request["batch"]))
+        channel.basic_ack(delivery_tag=method.delivery_tag)
+
+    def server_solve_(self):
+        """Top-k of (1/batches_number) sum_i V_i V_i^T in arrival order, implicit."""
+        bases = [linalg.require_device_tensor(e, "eigenspace") for e in self.computed_eigens]
+        Wt = linalg.stack_bases(bases)
+        return linalg.projavg_topk(Wt, int(self.rank), 1.0 / self.batches_number, q0=bases[0])
+
+    def send_to_slaves_(self, message):
+        print("Sending to slaves: ")
+        self.channel.basic_publish(exchange="", routing_key="slaves", body=message)
+
+
+def run_master(broker, rank, batches_number, data):
+    master = MasterNode(broker, rank, batches_number, data)
+    master.start()
+    return master
+
+
+def run_slave(broker, data):
+    slave = SlaveNode(broker, data)
+    slave.start()
+    return slave
+
+
+def run_local(rank, batches_number, data, broker_name="inproc-local"):
+    """Both roles in one process over the in-process broker (addition)."""
+    b = _broker.InProcBroker(broker_name)
+    SlaveNode(b, data)
+    master = MasterNode(b, rank, batches_number, data)
+    master.start()
+    return master
+
+
+def preprocess(data):
+    """distributed.py:170-173: grayscale (mean over RGB) and flatten to R^1024."""
+    data = data.mean(axis=3)
+    return data.reshape(data.shape[:-2] + (-1,))
+
+
+def main(argv=None):
+    parser = argparse.ArgumentParser(description="Multinode PCA")
+    parser.add_argument("--mode", help="Mode to run script - slave, master or local")
+    parser.add_argument("--broker", help="Message broker name (in-process broker)")
+    parser.add_argument("--rank", help="Approximation rank (only for master node")
+    parser.add_argument("--batches", help="Total batches number")
+    parser.add_argument("--data", default="cifar-10-batches-py", help="Path to dataset")
+    args = parser.parse_args(argv)
+    if args.broker is None:
+        raise RuntimeError("Broker not specified")
+    from .load_data import load_CIFAR_10_data
+    data, filenames, labels = load_CIFAR_10_data(args.data)
+    data = preprocess(data)
+    if args.mode == "slave":
+        return run_slave(args.broker, data)
+    elif args.mode == "master":
+        return run_master(args.broker, int(args.rank), int(args.batches), data)
+    elif args.mode == "local":
+        return run_local(int(args.rank), int(args.batches), data, args.broker)
+    raise RuntimeError("Mode not specified or specified wrong")
+
+
+if __name__ == "__main__":
+    main()

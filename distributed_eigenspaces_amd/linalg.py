@@ -1,0 +1,319 @@
+"""Device-level API of the hot path: PyTorch-ROCm tensors in, HIP kernels via the C ABI.
+
+Buffers are torch tensors on ``cuda:<i>`` (HIP under ROCm); PyTorch is used only
+for device memory, streams and collectives.  Every op launches on the current
+torch stream of the tensor's device and returns without a host sync, except the
+eigensolvers, which synchronise that stream between sweeps to test convergence
+(the reference's scipy.linalg.eigh is synchronous too).
+
+There is no CPU fallback: inputs must live on a ROCm device, and the ops raise
+if ``libdeig.so`` is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+import warnings
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+
+__all__ = [
+    "sigma_hat", "topk_eigh", "projavg_topk", "oja_step", "default_subspace",
+    "EigResult", "require_device_tensor", "project", "stack_bases",
+]
+
+DEFAULT_TOL = 1e-6
+DEFAULT_MAX_SWEEPS = 300
+
+
+@dataclass
+class EigResult:
+    """Top-k eigenpairs, ascending order (LAPACK / scipy.linalg.eigh convention)."""
+
+    evals: torch.Tensor   # (k,) float32
+    V: torch.Tensor       # (d, k) float32, column-major (Fortran) strides (1, d)
+    sweeps: int
+    resid: float          # max_j ||A v_j - lambda_j v_j|| / |lambda_max|
+    converged: bool
+
+
+# ---------------------------------------------------------------- workspace cache
+class _Workspace(threading.local):
+    def __init__(self):
+        self.bufs = {}
+
+
+_ws = _Workspace()
+
+
+def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
+    """Per-thread, per-device, per-stream grow-only uint8 workspace."""
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    buf = _ws.bufs.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        _ws.bufs[key] = buf
+    return buf
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device_tensor(t, name: str = "input") -> torch.Tensor:
+    """float32 tensor on a ROCm device (host arrays are copied over).  No CPU path."""
+    if not torch.cuda.is_available():
+        raise RuntimeError(
+            f"{name}: distributed_eigenspaces_amd runs only on a ROCm GPU (MI355X); "
+            "no GPU is visible and there is no CPU fallback")
+    if not isinstance(t, torch.Tensor):
+        t = torch.as_tensor(t)
+    if t.device.type != "cuda":
+        t = t.to(device=torch.device("cuda", torch.cuda.current_device()))
+    if t.dtype != torch.float32:
+        t = t.to(torch.float32)
+    return t
+
+
+def _rowmajor_4(t: torch.Tensor, name: str) -> torch.Tensor:
+    """2-D row-major view with unit column stride, row stride % 4 == 0, 16-B aligned."""
+    if t.dim() != 2:
+        raise ValueError(f"{name} must be 2-D, got shape {tuple(t.shape)}")
+    ok = (t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.stride(0) >= t.shape[1]
+          and t.data_ptr() % 16 == 0)
+    if ok:
+        return t
+    d = t.shape[1]
+    dp = (d + 3) // 4 * 4
+    out = torch.zeros((t.shape[0], dp), dtype=torch.float32, device=t.device)
+    out[:, :d] = t
+    return out
+
+
+def default_subspace(d: int, k: int) -> int:
+    return int(_lib.lib().deig_default_subspace(int(d), int(k)))
+
+
+# ---------------------------------------------------------------- covariance
+def sigma_hat(x: torch.Tensor, alpha: float | None = None,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    """Sigma_hat = alpha * X^T X with alpha = 1/n by default (uncentered).
+
+    GPU replacement for ``SlaveNode.compute_sigma_hat_`` (distributed.py:59-70).
+    x: (n, d) float32 on the GPU.  Returns a (d, d) float32 tensor, bit-exactly
+    symmetric.  Columns are zero-padded to a multiple of 4 internally if needed.
+    """
+    x = require_device_tensor(x, "sigma_hat")
+    if x.dim() != 2:
+        raise ValueError(f"x must be 2-D (n, d), got {tuple(x.shape)}")
+    n, d = x.shape
+    if n == 0:
+        # numpy: zeros / 0 -> NaN (with a RuntimeWarning); keep that behaviour
+        return torch.full((d, d), float("nan"), dtype=torch.float32, device=x.device)
+    a = (1.0 / n) if alpha is None else float(alpha)
+    xx = _rowmajor_4(x, "x")
+    dp = xx.shape[1]
+    if out is not None and dp == d and out.shape == (d, d) and out.is_contiguous() \
+            and out.dtype == torch.float32 and out.device == x.device and d % 4 == 0:
+        S = out
+    else:
+        S = torch.empty((dp, dp), dtype=torch.float32, device=x.device)
+    L = _lib.lib()
+    with torch.cuda.device(x.device):
+        nbytes = L.deig_syrk_workspace(n, dp)
+        ws = _workspace(x.device, nbytes) if nbytes else None
+        rc = L.deig_syrk_f32(xx.data_ptr(), n, dp, xx.stride(0), ctypes.c_float(a), S.data_ptr(),
+                             S.stride(0), ws.data_ptr() if ws is not None else None,
+                             nbytes, _stream(x.device))
+    _lib.check(rc, "deig_syrk_f32")
+    if dp != d:
+        S = S[:d, :d].contiguous()
+        if out is not None:
+            out.copy_(S)
+            return out
+    return S
+
+
+# ---------------------------------------------------------------- eigensolvers
+def _pad_dim(d: int) -> int:
+    return max(16, (d + 3) // 4 * 4)
+
+
+def _finish(rc, V, evals, sweeps, resid, what):
+    _lib.check(rc, what)
+    conv = rc == _lib.DEIG_OK
+    if not conv:
+        warnings.warn(f"{what}: {_lib.last_error()}", _lib.NotConvergedWarning, stacklevel=3)
+    return EigResult(evals=evals, V=V, sweeps=int(sweeps.value), resid=float(resid.value),
+                     converged=conv)
+
+
+def _colmajor(d: int, k: int, device) -> torch.Tensor:
+    return torch.empty((k, d), dtype=torch.float32, device=device).t()
+
+
+def _warm(q0, d, device):
+    if q0 is None:
+        return None, 0, d
+    q = require_device_tensor(q0, "q0")
+    if q.dim() == 1:
+        q = q[:, None]
+    if q.shape[0] != d:
+        raise ValueError(f"q0 must have {d} rows")
+    q = q.t().contiguous().t()  # column-major
+    return q, q.shape[1], q.stride(1)
+
+
+def topk_eigh(S: torch.Tensor, k: int, *, p: int | None = None, tol: float = DEFAULT_TOL,
+              max_sweeps: int = DEFAULT_MAX_SWEEPS, q0: torch.Tensor | None = None,
+              check_finite: bool = True) -> EigResult:
+    """Top-k eigenpairs of a symmetric matrix, ascending (GPU subspace iteration).
+
+    GPU replacement for ``Node.top_k_eigenvectors`` (distributed.py:22-29:
+    ``eigh(matrix, eigvals=(N-k, N-1))[1]``) that also returns the eigenvalues.
+    Only the lower triangle matters mathematically, but the full matrix is read
+    (the SYRK output is bit-exactly symmetric).  Raises ValueError for k outside
+    [1, d] like scipy's subset_by_index check.
+    """
+    S = require_device_tensor(S, "topk_eigh")
+    if S.dim() != 2 or S.shape[0] != S.shape[1]:
+        raise ValueError(f"expected a square matrix, got {tuple(S.shape)}")
+    d = S.shape[0]
+    k = int(k)
+    if not 1 <= k <= d:
+        raise ValueError(f"k={k} out of range [1, {d}]")
+    if check_finite and not bool(torch.isfinite(S).all()):
+        raise ValueError("array must not contain infs or NaNs")
+    dp = _pad_dim(d)
+    if dp != d or S.stride(1) != 1 or S.stride(0) % 4 or S.data_ptr() % 16:
+        Sp = torch.zeros((dp, dp), dtype=torch.float32, device=S.device)
+        Sp[:d, :d] = S
+        S = Sp
+    q, k0, ldq = _warm(q0, d, S.device)
+    if q is not None and dp != d:
+        qp = torch.zeros((dp, k0), dtype=torch.float32, device=S.device)
+        qp[:d] = q
+        q, ldq = qp.t().contiguous().t(), dp
+    pp = int(p) if p else default_subspace(dp, k)
+    V = _colmajor(dp, k, S.device)
+    evals = torch.empty(k, dtype=torch.float32, device=S.device)
+    sweeps, resid = ctypes.c_int(0), ctypes.c_float(0)
+    L = _lib.lib()
+    with torch.cuda.device(S.device):
+        nbytes = L.deig_topk_workspace(dp, k, pp)
+        ws = _workspace(S.device, nbytes)
+        rc = L.deig_topk_sym_f32(S.data_ptr(), dp, S.stride(0), k, pp, int(max_sweeps),
+                                 ctypes.c_float(tol), q.data_ptr() if q is not None else None,
+                                 k0, ldq, V.data_ptr(), dp, evals.data_ptr(),
+                                 ctypes.byref(sweeps), ctypes.byref(resid), ws.data_ptr(),
+                                 nbytes, _stream(S.device))
+    res = _finish(rc, V, evals, sweeps, resid, "deig_topk_sym_f32")
+    if dp != d:
+        res.V = res.V[:d].t().contiguous().t()
+    return res
+
+
+def stack_bases(bases) -> torch.Tensor:
+    """[V_1, ..., V_m] (each d x k) -> Wt = [V_1^T; ...; V_m^T]  ((m k) x d row-major)."""
+    rows = [require_device_tensor(v, "basis").t() for v in bases]
+    return torch.cat(rows, dim=0).contiguous()
+
+
+def projavg_topk(Wt: torch.Tensor, k: int, scale: float, *, p: int | None = None,
+                 tol: float = DEFAULT_TOL, max_sweeps: int = DEFAULT_MAX_SWEEPS,
+                 q0: torch.Tensor | None = None) -> EigResult:
+    """Top-k eigenpairs of scale * sum_i V_i V_i^T, never forming the d x d matrix.
+
+    GPU replacement for MasterNode.callback_ (distributed.py:126-130:
+    sigma_tilde = sum V V^T / batches_number) followed by the notebook's server
+    solve (Online Distributed PCA.ipynb raw line 306).  Wt = stack_bases(...)
+    is (m k) x d row-major; rows may carry per-basis weights (online variant).
+    """
+    Wt = require_device_tensor(Wt, "projavg_topk")
+    if Wt.dim() != 2:
+        raise ValueError("Wt must be 2-D ((m k) x d)")
+    mk, d = Wt.shape
+    k = int(k)
+    if not 1 <= k <= d:
+        raise ValueError(f"k={k} out of range [1, {d}]")
+    dp = _pad_dim(d)
+    if dp != d or Wt.stride(1) != 1 or Wt.stride(0) % 4 or Wt.data_ptr() % 16:
+        Wp = torch.zeros((mk, dp), dtype=torch.float32, device=Wt.device)
+        Wp[:, :d] = Wt
+        Wt = Wp
+    q, k0, ldq = _warm(q0, d, Wt.device)
+    if q is not None and dp != d:
+        qp = torch.zeros((dp, k0), dtype=torch.float32, device=Wt.device)
+        qp[:d] = q
+        q, ldq = qp.t().contiguous().t(), dp
+    pp = int(p) if p else default_subspace(dp, k)
+    V = _colmajor(dp, k, Wt.device)
+    evals = torch.empty(k, dtype=torch.float32, device=Wt.device)
+    sweeps, resid = ctypes.c_int(0), ctypes.c_float(0)
+    L = _lib.lib()
+    with torch.cuda.device(Wt.device):
+        nbytes = L.deig_projavg_workspace(dp, mk, k, pp)
+        ws = _workspace(Wt.device, nbytes)
+        rc = L.deig_projavg_topk_f32(Wt.data_ptr(), dp, mk, Wt.stride(0), ctypes.c_float(scale),
+                                     k, pp, int(max_sweeps), ctypes.c_float(tol),
+                                     q.data_ptr() if q is not None else None, k0, ldq,
+                                     V.data_ptr(), dp, evals.data_ptr(), ctypes.byref(sweeps),
+                                     ctypes.byref(resid), ws.data_ptr(), nbytes,
+                                     _stream(Wt.device))
+    res = _finish(rc, V, evals, sweeps, resid, "deig_projavg_topk_f32")
+    if dp != d:
+        res.V = res.V[:d].t().contiguous().t()
+    return res
+
+
+# ---------------------------------------------------------------- Oja
+def oja_step(Xb: torch.Tensor, V: torch.Tensor, eta: float) -> torch.Tensor:
+    """In-place mini-batch Oja update V <- orth(V + eta/b Xb^T Xb V) (config 4).
+
+    Not in the reference (parity unpinned).  V: (d, k) column-major float32
+    (as returned by topk_eigh), k <= 64.  Returns V.
+    """
+    Xb = _rowmajor_4(require_device_tensor(Xb, "oja_step"), "Xb")
+    b, d = Xb.shape
+    if V.dim() != 2 or V.shape[0] != d or V.stride(0) != 1 or V.dtype != torch.float32 \
+            or V.device != Xb.device:
+        raise ValueError("V must be a (d, k) column-major float32 tensor on Xb's device")
+    k = V.shape[1]
+    L = _lib.lib()
+    with torch.cuda.device(Xb.device):
+        nbytes = L.deig_oja_workspace(b, d, k)
+        ws = _workspace(Xb.device, nbytes)
+        rc = L.deig_oja_step_f32(Xb.data_ptr(), b, d, Xb.stride(0), ctypes.c_float(eta),
+                                 V.data_ptr(), k, V.stride(1), ws.data_ptr(), nbytes,
+                                 _stream(Xb.device))
+    _lib.check(rc, "deig_oja_step_f32")
+    return V
+
+
+# ---------------------------------------------------------------- projection
+def project(X: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
+    """Y = X W  (NB:345 ``X @ matrix_w``): X (n, d) row-major, W (d, k) any layout."""
+    X = _rowmajor_4(require_device_tensor(X, "project"), "X")
+    W = require_device_tensor(W, "matrix_w")
+    n, dp = X.shape
+    d, k = W.shape
+    if d > dp or (dp != d and dp != (d + 3) // 4 * 4):
+        raise ValueError(f"shape mismatch: X has {dp} columns, W has {d} rows")
+    if dp != d:
+        Wp = torch.zeros((dp, k), dtype=torch.float32, device=W.device)
+        Wp[:d] = W
+        W = Wp
+    W = W.t().contiguous().t()  # column-major
+    Y = torch.empty((n, k), dtype=torch.float32, device=X.device)
+    L = _lib.lib()
+    with torch.cuda.device(X.device):
+        nbytes = L.deig_project_workspace(n, dp, k)
+        ws = _workspace(X.device, nbytes)
+        rc = L.deig_project_f32(X.data_ptr(), n, dp, X.stride(0), W.data_ptr(), k, W.stride(1),
+                                Y.data_ptr(), Y.stride(0), ws.data_ptr(), nbytes,
+                                _stream(X.device))
+    _lib.check(rc, "deig_project_f32")
+    return Y

@@ -1,0 +1,108 @@
+/*
+ * deig.h - C ABI of libdeig.so, the MI355X (gfx950) hot path of the distributed
+ * eigenspace estimator (TimeEscaper/distributed_eigenspaces).
+ *
+ * Every entry point takes raw device pointers, sizes and leading dimensions (in
+ * elements), caller-provided device workspace and a hipStream_t (passed as
+ * void*).  The library never allocates or frees device memory and keeps no
+ * global mutable state except a thread-local error string.  Work is enqueued on
+ * the given stream; entry points that iterate (the eigensolvers) synchronise that
+ * stream between sweeps to test convergence, and return when done.
+ *
+ * Layouts: sample matrices X are row-major n x d (row stride ldx); symmetric
+ * matrices S are row-major d x d (full storage, both triangles written); bases V
+ * are COLUMN-major d x k (Fortran order, column stride ldv), columns in ASCENDING
+ * eigenvalue order, exactly like LAPACK ?syevr / scipy.linalg.eigh.  A stack of m
+ * bases is passed as Wt = [V_1^T; ...; V_m^T], i.e. (m*k) x d row-major, which is
+ * the byte layout of m column-major d x k bases laid end to end.
+ *
+ * Return codes: 0 ok; DEIG_NOT_CONVERGED (1) = results written but the residual
+ * test did not pass within max_sweeps; negative = error (see deig_last_error()).
+ */
+#ifndef DEIG_H
+#define DEIG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DEIG_OK 0
+#define DEIG_NOT_CONVERGED 1
+#define DEIG_EINVAL (-1)
+#define DEIG_EHIP (-2)
+#define DEIG_EWORKSPACE (-3)
+
+/* Library version, e.g. 0x000100 for 0.1.0. */
+int deig_version(void);
+
+/* Thread-local message for the last nonzero return on this thread ("" if none). */
+const char* deig_last_error(void);
+
+/* Sigma_hat = alpha * X^T X  (alpha = 1/n reproduces the reference).
+ * Replaces SlaveNode.compute_sigma_hat_  distributed.py:59-70
+ * (np.zeros((d,d)) += np.dot(x.T, x); /= n  ->  OpenBLAS dsyrk).
+ * fp32 in, fp32 MFMA accumulate; output is bit-exactly symmetric.
+ * Requires n >= 1, d % 4 == 0, ldx % 4 == 0, lds % 4 == 0, 16-byte aligned X, S. */
+int deig_syrk_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha,
+                  float* S, int64_t lds, void* ws, size_t ws_bytes, void* stream);
+size_t deig_syrk_workspace(int64_t n, int64_t d);
+
+/* Subspace size the solvers use for a given k when the caller passes p <= 0. */
+int deig_default_subspace(int64_t d, int k);
+
+/* Top-k eigenpairs of a dense symmetric S (d x d, row-major, lds), ascending.
+ * Replaces Node.top_k_eigenvectors  distributed.py:22-29
+ * (scipy.linalg.eigh(S, eigvals=(d-k, d-1))[1]  ->  LAPACK dsyevr), plus the
+ * eigenvalues ([0] of the same call) as a side output.
+ * Block subspace iteration with Rayleigh-Ritz on a p-dimensional subspace
+ * (k <= p <= 128, p % 16 == 0, p <= d).  Q0 (d x k0 column-major, ldq0) is an
+ * optional warm start (NULL / k0 = 0 -> deterministic pseudo-random start).
+ * Stops when max_j ||S v_j - lambda_j v_j|| <= tol * |lambda_max| or the
+ * residual stagnates, after at most max_sweeps sweeps.
+ * Outputs: V (d x k col-major, ldv), evals (k, ascending), *sweeps_out,
+ * *resid_out = final max relative residual (host pointers, may be NULL). */
+int deig_topk_sym_f32(const float* S, int64_t d, int64_t lds, int k, int p,
+                      int max_sweeps, float tol, const float* Q0, int k0, int64_t ldq0,
+                      float* V, int64_t ldv, float* evals, int* sweeps_out,
+                      float* resid_out, void* ws, size_t ws_bytes, void* stream);
+size_t deig_topk_workspace(int64_t d, int k, int p);
+
+/* Server solve: top-k eigenpairs of  scale * sum_i V_i V_i^T  without forming it.
+ * Wt = [V_1^T; ...; V_m^T] is (mk) x d row-major (ldw); scale = 1/batches_number.
+ * Replaces MasterNode.callback_  distributed.py:126-130 (sigma_tilde += V V^T;
+ * /= batches_number) + the notebook's server solve (Online Distributed
+ * PCA.ipynb raw line 306: top_k_eigenvectors(segma_bar, k)).  Same solver and
+ * outputs as deig_topk_sym_f32; the operator is Q -> scale * Wt^T (Wt Q). */
+int deig_projavg_topk_f32(const float* Wt, int64_t d, int64_t mk, int64_t ldw,
+                          float scale, int k, int p, int max_sweeps, float tol,
+                          const float* Q0, int k0, int64_t ldq0, float* V, int64_t ldv,
+                          float* evals, int* sweeps_out, float* resid_out, void* ws,
+                          size_t ws_bytes, void* stream);
+size_t deig_projavg_workspace(int64_t d, int64_t mk, int k, int p);
+
+/* One mini-batch Oja step (online variant, BASELINE.json config 4; not in the
+ * reference - parity unpinned):  V <- orth(V + eta/b * Xb^T (Xb V)).
+ * Xb is b x d row-major (ldx), V is d x k column-major (ldv), updated in place.
+ * k <= 64.  Orthonormalisation: Cholesky-QR2. */
+int deig_oja_step_f32(const float* Xb, int64_t b, int64_t d, int64_t ldx, float eta,
+                      float* V, int k, int64_t ldv, void* ws, size_t ws_bytes,
+                      void* stream);
+size_t deig_oja_workspace(int64_t b, int64_t d, int k);
+
+/* Projection onto an estimated eigenspace: Y = X W.
+ * Replaces the notebook's  online_distributed_PCA = lambda X: X @ matrix_w
+ * (Online Distributed PCA.ipynb raw line 345).  X: n x d row-major (ldx), W: d x k
+ * column-major (ldw, the solvers' V), Y: n x k row-major (ldy).  k <= 256. */
+int deig_project_f32(const float* X, int64_t n, int64_t d, int64_t ldx, const float* W, int k,
+                     int64_t ldw, float* Y, int64_t ldy, void* ws, size_t ws_bytes,
+                     void* stream);
+size_t deig_project_workspace(int64_t n, int64_t d, int k);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DEIG_H */
