@@ -57,8 +57,9 @@ def grayscale_flatten(images):
     """(N, 32, 32, 3) -> (N, 1024) float32 on the GPU: mean over channels, flatten.
 
     Same values as ``data.mean(axis=3).reshape(N, -1)`` (distributed.py:171-173)
-    rounded to fp32 (the mean of three uint8 values is computed exactly in fp32
-    before the division)."""
+    rounded once to fp32: the channel sum is exact and the division is done in
+    float64 on the device, then rounded (fp32 division on the device is not
+    correctly rounded)."""
     import torch
 
     from .linalg import require_device_tensor
@@ -67,5 +68,5 @@ def grayscale_flatten(images):
     if not torch.cuda.is_available():
         raise RuntimeError("grayscale_flatten runs on the GPU (no CPU fallback)")
     x = images.to(device=torch.device("cuda", torch.cuda.current_device()))
-    x = x.to(torch.float32).sum(dim=3) / 3.0
+    x = (x.to(torch.float64).sum(dim=3) / 3.0).to(torch.float32)
     return require_device_tensor(x.reshape(x.shape[0], -1), "images")

@@ -25,7 +25,7 @@ __all__ = [
     "sigma_hat", "top_k_eigh", "top_k_eigenvectors", "split_batches",
     "dispatch_order", "projector_average", "server_topk", "make_batches",
     "online_notebook", "online_figure", "one_shot", "oja_epoch",
-    "projector_distance", "sin_theta",
+    "projector_distance", "sin_theta", "align_signs",
 ]
 
 
@@ -181,6 +181,14 @@ def projector_distance(A, B) -> float:
     aa, bb, ab = A.T @ A, B.T @ B, A.T @ B
     val = np.sum(aa * aa) + np.sum(bb * bb) - 2.0 * np.sum(ab * ab)
     return float(np.sqrt(max(val, 0.0)))
+
+
+def align_signs(V, ref):
+    """Flip the sign of each column of V to match ref (eigenvectors are sign-ambiguous)."""
+    V = np.array(V, dtype=np.float64)
+    s = np.sign(np.sum(V * np.asarray(ref, dtype=np.float64), axis=0))
+    s[s == 0] = 1.0
+    return V * s
 
 
 def sin_theta(A, B) -> float:

@@ -1,0 +1,59 @@
+"""The C-ABI library loads and exports every symbol include/deig.h declares (CPU)."""
+import ctypes
+
+import pytest
+
+from distributed_eigenspaces_amd import _lib
+
+
+def test_header_symbols_exported():
+    L = _lib.lib()
+    syms = _lib.header_symbols()
+    assert len(syms) >= 13
+    for s in syms:
+        assert hasattr(L, s), f"libdeig.so does not export {s}"
+        assert s in _lib.SIGNATURES, f"no ctypes signature for {s}"
+
+
+def test_version_and_error_string():
+    L = _lib.lib()
+    assert L.deig_version() == 0x000100
+    assert isinstance(_lib.last_error(), str)
+
+
+def test_workspace_queries():
+    L = _lib.lib()
+    # config-3 shard: d=8192 -> 528 tiles = 2 x 256 + 16 remainder tiles -> 2 slabs/CU
+    assert L.deig_syrk_workspace(1 << 21, 8192) == 2 * 256 * 256 * 256 * 4
+    assert L.deig_syrk_workspace(1000, 256) > 0
+    for d, k in [(64, 4), (3072, 16), (8192, 64), (16384, 128)]:
+        p = L.deig_default_subspace(d, k)
+        assert p % 16 == 0 and k <= p <= 128
+        assert L.deig_topk_workspace(d, k, 0) >= d * 2 * p * 4
+        assert L.deig_projavg_workspace(d, 8 * k, k, 0) > 0
+    assert L.deig_oja_workspace(4096, 3072, 32) > 3072 * 32 * 4
+    assert L.deig_project_workspace(60000, 1024, 2) > 0
+
+
+def test_invalid_arguments_rejected_before_any_gpu_work():
+    L = _lib.lib()
+    rc = L.deig_syrk_f32(None, 0, 64, 64, ctypes.c_float(1.0), None, 64, None, 0, None)
+    assert rc == _lib.DEIG_EINVAL and "n must be" in _lib.last_error()
+    rc = L.deig_syrk_f32(None, 10, 6, 8, ctypes.c_float(1.0), None, 8, None, 0, None)
+    assert rc == _lib.DEIG_EINVAL
+    with pytest.raises(ValueError):
+        _lib.check(_lib.DEIG_EINVAL, "x")
+    with pytest.raises(_lib.DeigError):
+        _lib.check(_lib.DEIG_EHIP, "x")
+
+
+def test_no_cpu_fallback():
+    import torch
+
+    import distributed_eigenspaces_amd as de
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        de.sigma_hat(torch.ones(4, 4))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        de.topk_eigh(torch.eye(16), 2)
