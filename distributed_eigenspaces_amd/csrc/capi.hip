@@ -3,6 +3,7 @@
 // device memory is caller-provided (PyTorch tensors on the Python side).
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "deig_internal.hpp"
@@ -126,6 +127,7 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
   if (!ws || total > ws_bytes)
     return fail(DEIG_EWORKSPACE, "solver: workspace %zu bytes < required %zu", ws_bytes, total);
 
+  static const bool debug = getenv("DEIG_DEBUG") && getenv("DEIG_DEBUG")[0] == '1';
   int rc = rr_init_launch(w.rr.Z, d, p, Q0, k0, ldq0, 0x5eed5eedull, st);
   if (rc) return rc;
   float best = 3.4e38f;
@@ -142,6 +144,12 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
     if ((rc = rr_update_launch(w.rr, d, p, k, V, ldv, evals, st))) return rc;
     DEIG_HIP_CHECK(hipMemcpyAsync(&last, w.rr.resid + k, sizeof(float), hipMemcpyDeviceToHost, st));
     DEIG_HIP_CHECK(hipStreamSynchronize(st));
+    if (debug) {
+      int inf[3] = {0, 0, 0};
+      DEIG_HIP_CHECK(hipMemcpy(inf, w.rr.info, sizeof(inf), hipMemcpyDeviceToHost));
+      fprintf(stderr, "[deig] d=%lld k=%d p=%d sweep %d resid %.3e chol_floor %d jacobi_sweeps %d rotations %d\n",
+              (long long)d, k, p, it + 1, last, inf[0], inf[1], inf[2]);
+    }
     if (!(last == last)) {  // NaN
       if (sweeps_out) *sweeps_out = it + 1;
       if (resid_out) *resid_out = last;

@@ -69,36 +69,41 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 }
 
 __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ Cg, int p,
-                                                      float* __restrict__ Linv_g,
-                                                      float* __restrict__ Wtmp_g,
                                                       float* __restrict__ Wout,
                                                       float* __restrict__ lam_out,
                                                       float* __restrict__ cs_out,
                                                       int* __restrict__ info, int max_jsweeps) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int pp = p * p;
+  const int half = p >> 1;
   float* X1 = sm;
   float* X2 = sm + pp;
   float* dsc = X2 + pp;   // p
-  float* gam = dsc + p;   // p
-  float* sig = gam + p;   // p
-  float* lamv = sig + p;  // p
+  float* lamv = dsc + p;  // p
   float* gd = lamv + p;   // p
-  int* part = reinterpret_cast<int*>(gd + p);  // p
-  int* rank = part + p;                        // p
+  float* pc = gd + p;     // p/2 rotation cosines
+  float* ps = pc + half;  // p/2 rotation sines
+  int* pa = reinterpret_cast<int*>(ps + half);  // p/2
+  int* pb = pa + half;                          // p/2
+  int* rank = pb + half;                        // p
   float* red = reinterpret_cast<float*>(rank + p);  // RT/64 + 2
+  int* nrot = reinterpret_cast<int*>(red + RT / 64 + 2);
   const int tid = threadIdx.x;
   const int ldc = 2 * p;
   const float* Mg = Cg;
   const float* Hg = Cg + p;
   const float* Gg = Cg + (int64_t)p * ldc + p;
 
-  // ---- 0. column scaling of Q
+  // ---- 0. D = diag(M)^-1/2;  X1 = D M D
   for (int a = tid; a < p; a += RT) {
     const float m = Mg[a * ldc + a];
     dsc[a] = (m > 0.f && isfinite(m)) ? rsqrtf(m) : 1.0f;
   }
-  if (tid == 0) info[0] = 0;
+  if (tid == 0) {
+    info[0] = 0;
+    info[1] = 0;
+    info[2] = 0;
+  }
   __syncthreads();
   for (int idx = tid; idx < pp; idx += RT) {
     const int a = idx / p, b = idx - a * p;
@@ -140,52 +145,86 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
     }
     __syncthreads();
   }
-  for (int idx = tid; idx < pp; idx += RT) Linv_g[idx] = X2[idx];
-  __syncthreads();
 
-  // ---- 3. T1 = L^-1 (D H D) -> X1
+  // ---- 3. X1 = D H D ; 4. X1 = L^-1 X1 ; 5. X1 = X1 L^-T  (register-staged)
   for (int idx = tid; idx < pp; idx += RT) {
     const int a = idx / p, b = idx - a * p;
-    float s = 0.f;
-    for (int t = 0; t <= a; ++t) s += X2[a * p + t] * (Hg[t * ldc + b] * dsc[t]);
-    X1[idx] = s * dsc[b];
+    X1[idx] = Hg[a * ldc + b] * dsc[a] * dsc[b];
   }
   __syncthreads();
-  // ---- 4. H~ = T1 L^-T -> X2   (L^-1 re-read from global; X2 is overwritten)
-  for (int idx = tid; idx < pp; idx += RT) {
-    const int a = idx / p, b = idx - a * p;
-    float s = 0.f;
-    for (int t = 0; t <= b; ++t) s += X1[a * p + t] * Linv_g[b * p + t];
-    X2[idx] = s;
+  float nv[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int idx = tid + u * RT;
+    nv[u] = 0.f;
+    if (idx < pp) {
+      const int a = idx / p, b = idx - a * p;
+      float s = 0.f;
+      for (int t = 0; t <= a; ++t) s = fmaf(X2[a * p + t], X1[t * p + b], s);
+      nv[u] = s;
+    }
   }
   __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int idx = tid + u * RT;
+    if (idx < pp) X1[idx] = nv[u];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int idx = tid + u * RT;
+    nv[u] = 0.f;
+    if (idx < pp) {
+      const int a = idx / p, b = idx - a * p;
+      float s = 0.f;
+      for (int t = 0; t <= b; ++t) s = fmaf(X1[a * p + t], X2[b * p + t], s);
+      nv[u] = s;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int idx = tid + u * RT;
+    if (idx < pp) X1[idx] = nv[u];
+  }
+  __syncthreads();
+  // symmetrise H~ and turn X2 = L^-1 into the eigenvector accumulator V0 = L^-T:
+  // every Jacobi rotation right-multiplies it, so at the end X2 = L^-T U.
   for (int idx = tid; idx < pp; idx += RT) {
     const int a = idx / p, b = idx - a * p;
     if (a < b) {
-      const float v = 0.5f * (X2[a * p + b] + X2[b * p + a]);
-      X2[a * p + b] = v;
-      X2[b * p + a] = v;
+      const float v = 0.5f * (X1[a * p + b] + X1[b * p + a]);
+      X1[a * p + b] = v;
+      X1[b * p + a] = v;
+      const float l = X2[b * p + a];  // L^-1 is lower: (b, a) holds the value
+      X2[a * p + b] = l;
+      X2[b * p + a] = 0.f;
     }
-  }
-  for (int idx = tid; idx < pp; idx += RT) {
-    const int a = idx / p, b = idx - a * p;
-    X1[idx] = (a == b) ? 1.0f : 0.0f;
   }
   __syncthreads();
 
-  // ---- 5. parallel cyclic Jacobi on X2; eigenvectors accumulate in X1 (columns)
-  const int half = p >> 1;
+  // ---- 6. parallel cyclic Jacobi on X1 (round-robin pairs; each thread owns a 2x2
+  //         block of the rotated matrix, updated in place from one read).
+  // nrot[0]: rotations in this sweep; nrot[1], nrot[2]: per-step counters used on
+  // alternating steps, so a counter is only reset after every thread has read it.
+  if (tid == 0) {
+    nrot[1] = 0;
+    nrot[2] = 0;
+  }
   for (int sw = 0; sw < max_jsweeps; ++sw) {
-    float off = 0.f, dg = 0.f;
-    for (int idx = tid; idx < pp; idx += RT) {
-      const int a = idx / p, b = idx - a * p;
-      const float v = X2[idx];
-      if (a == b) dg += v * v; else off += v * v;
-    }
-    off = block_sum(off, red);
-    dg = block_sum(dg, red);
-    if (off <= 1e-14f * dg) break;
+    if (tid == 0) nrot[0] = 0;
+    // scale for the absolute rotation threshold
+    float dmax = 0.f;
+    for (int a = tid; a < p; a += RT) dmax = fmaxf(dmax, fabsf(X1[a * p + a]));
+    for (int o = 32; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o, 64));
+    if ((tid & 63) == 0) red[tid >> 6] = dmax;
+    __syncthreads();
+    float amax = 0.f;
+    for (int i = 0; i < RT / 64; ++i) amax = fmaxf(amax, red[i]);
+    const float abs_thr = 1e-9f * amax;
     for (int st = 0; st < p - 1; ++st) {
+      const int ci = 1 + (st & 1);
       if (tid < half) {
         int a, b;
         if (tid == 0) {
@@ -195,76 +234,94 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
           a = (st + tid) % (p - 1);
           b = (st - tid + (p - 1)) % (p - 1);
         }
-        const float app = X2[a * p + a], aqq = X2[b * p + b], apq = X2[a * p + b];
+        const float app = X1[a * p + a], aqq = X1[b * p + b], apq = X1[a * p + b];
         float c = 1.f, s = 0.f;
-        if (fabsf(apq) > 1e-30f && fabsf(apq) > 1e-9f * sqrtf(fabsf(app * aqq))) {
+        if (fabsf(apq) > abs_thr && fabsf(apq) > 2e-7f * sqrtf(fabsf(app * aqq))) {
           const float tau = (aqq - app) / (2.f * apq);
           const float t = (fabsf(tau) > 1e18f)
                               ? 0.5f / tau
                               : copysignf(1.f, tau) / (fabsf(tau) + sqrtf(1.f + tau * tau));
           c = rsqrtf(1.f + t * t);
           s = t * c;
+          atomicAdd(nrot + ci, 1);
         }
-        gam[a] = c; sig[a] = -s; part[a] = b;
-        gam[b] = c; sig[b] = s;  part[b] = a;
+        pa[tid] = a; pb[tid] = b; pc[tid] = c; ps[tid] = s;
       }
       __syncthreads();
-      float nv[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int idx = tid + u * RT;
-        nv[u] = 0.f;
-        if (idx < pp) {
-          const int r = idx / p, c = idx - r * p;
-          const int r2 = part[r], c2 = part[c];
-          const float gr = gam[r], sr = sig[r], gc = gam[c], sc = sig[c];
-          nv[u] = gr * (gc * X2[r * p + c] + sc * X2[r * p + c2]) +
-                  sr * (gc * X2[r2 * p + c] + sc * X2[r2 * p + c2]);
+      const int step_rot = nrot[ci];
+      if (step_rot != 0) {  // wave-uniform: identity steps apply nothing
+        for (int idx = tid; idx < half * half; idx += RT) {
+          const int tr = idx / half, tc = idx - tr * half;
+          const int ar = pa[tr], br = pb[tr], ac = pa[tc], bc = pb[tc];
+          const float cr = pc[tr], sr = ps[tr], cc = pc[tc], sc = ps[tc];
+          const float x = X1[ar * p + ac], y = X1[ar * p + bc];
+          const float z = X1[br * p + ac], w = X1[br * p + bc];
+          // columns: col_a' = c col_a - s col_b ; col_b' = s col_a + c col_b
+          const float x1 = cc * x - sc * y, y1 = sc * x + cc * y;
+          const float z1 = cc * z - sc * w, w1 = sc * z + cc * w;
+          // rows
+          X1[ar * p + ac] = cr * x1 - sr * z1;
+          X1[br * p + ac] = sr * x1 + cr * z1;
+          X1[ar * p + bc] = cr * y1 - sr * w1;
+          X1[br * p + bc] = sr * y1 + cr * w1;
+        }
+        for (int idx = tid; idx < p * half; idx += RT) {
+          const int r = idx / half, t = idx - r * half;
+          const int a = pa[t], b = pb[t];
+          const float c = pc[t], s = ps[t];
+          const float va = X2[r * p + a], vb = X2[r * p + b];
+          X2[r * p + a] = c * va - s * vb;
+          X2[r * p + b] = s * va + c * vb;
         }
       }
-      // eigenvector columns: V[:, x] <- gam_x V[:, x] + sig_x V[:, partner(x)]
-      for (int idx = tid; idx < p * half; idx += RT) {
-        const int r = idx / half, t = idx - r * half;
-        int a = (t == 0) ? p - 1 : (st + t) % (p - 1);
-        const int b = part[a];
-        const float va = X1[r * p + a], vb = X1[r * p + b];
-        X1[r * p + a] = gam[a] * va + sig[a] * vb;
-        X1[r * p + b] = gam[b] * vb + sig[b] * va;
-      }
       __syncthreads();
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int idx = tid + u * RT;
-        if (idx < pp) X2[idx] = nv[u];
+      if (tid == 0) {
+        nrot[0] += step_rot;
+        nrot[ci] = 0;
       }
-      __syncthreads();
     }
+    __syncthreads();
+    const int swrot = nrot[0];
+    if (tid == 0) {
+      info[1] = sw + 1;
+      info[2] += swrot;
+    }
+    __syncthreads();
+    if (swrot == 0) break;
   }
 
-  // ---- 6. W = D L^-T U -> Wtmp_g ; eigenvalues -> lamv
-  for (int a = tid; a < p; a += RT) lamv[a] = X2[a * p + a];
+  // ---- 7. eigenvalues; W = D (L^-T U)  (row scaling, in place in X2)
+  for (int a = tid; a < p; a += RT) lamv[a] = X1[a * p + a];
+  __syncthreads();
   for (int idx = tid; idx < pp; idx += RT) {
-    const int a = idx / p, j = idx - a * p;
-    float s = 0.f;
-    for (int t = a; t < p; ++t) s += Linv_g[t * p + a] * X1[t * p + j];
-    Wtmp_g[idx] = s * dsc[a];
+    const int a = idx / p, b = idx - a * p;
+    X2[idx] *= dsc[a];
+    X1[idx] = Gg[a * ldc + b];
   }
   __syncthreads();
-  for (int idx = tid; idx < pp; idx += RT) X1[idx] = Wtmp_g[idx];
+  // ---- 8. g_j = w_j^T G w_j
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int idx = tid + u * RT;
+    nv[u] = 0.f;
+    if (idx < pp) {
+      const int a = idx / p, j = idx - a * p;
+      float s = 0.f;
+      for (int b = 0; b < p; ++b) s = fmaf(X1[a * p + b], X2[b * p + j], s);
+      nv[u] = s * X2[idx];
+    }
+  }
   __syncthreads();
-  // ---- 7. g_j = w_j^T G w_j
-  for (int idx = tid; idx < pp; idx += RT) {
-    const int a = idx / p, j = idx - a * p;
-    float s = 0.f;
-    for (int b = 0; b < p; ++b) s += Gg[a * ldc + b] * X1[b * p + j];
-    X2[idx] = s;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int idx = tid + u * RT;
+    if (idx < pp) X1[idx] = nv[u];
   }
   __syncthreads();
   for (int j = tid; j < p; j += RT) {
     float s = 0.f;
-    for (int a = 0; a < p; ++a) s += X1[a * p + j] * X2[a * p + j];
+    for (int a = 0; a < p; ++a) s += X1[a * p + j];
     gd[j] = s;
-    // rank for descending order (ties by index)
     const float lj = lamv[j];
     int rk = 0;
     for (int b = 0; b < p; ++b) {
@@ -288,7 +345,7 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
   }
   for (int idx = tid; idx < pp; idx += RT) {
     const int a = idx / p, j = idx - a * p;
-    Wout[a * p + rank[j]] = X1[idx];
+    Wout[a * p + rank[j]] = X2[idx];
   }
 }
 
@@ -299,11 +356,13 @@ __global__ __launch_bounds__(256) void rr_update_kernel(float* __restrict__ Z, i
                                                         float* __restrict__ V, int64_t ldv,
                                                         float* __restrict__ resid_part) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* Ws = sm;              // p x p
-  float* Zs = sm + p * p;      // UR x 2p
+  float* Ws = sm;                  // p x p
+  float* Zs = sm + p * p;          // UR x 2p
+  float* rp = Zs + UR * 2 * p;     // ngrp x k partial residuals
   const int tid = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * UR;
   const int ld = 2 * p;
+  const int ngrp = 256 / p;        // row groups (p <= 128 -> >= 2)
   for (int idx = tid; idx < p * p; idx += 256) Ws[idx] = W[idx];
   for (int idx = tid; idx < UR * ld; idx += 256) {
     const int rr = idx / ld, c = idx - rr * ld;
@@ -311,10 +370,11 @@ __global__ __launch_bounds__(256) void rr_update_kernel(float* __restrict__ Z, i
     Zs[idx] = (row < d) ? Z[row * ld + c] : 0.f;
   }
   __syncthreads();
-  for (int j = tid; j < p; j += 256) {
+  const int grp = tid / p, j = tid - grp * p;
+  if (grp < ngrp) {
     const float lj = lam[j], cj = cs[j];
     float racc = 0.f;
-    for (int rr = 0; rr < UR; ++rr) {
+    for (int rr = grp; rr < UR; rr += ngrp) {
       const int64_t row = r0 + rr;
       if (row >= d) break;
       const float* zq = Zs + rr * ld;
@@ -332,38 +392,45 @@ __global__ __launch_bounds__(256) void rr_update_kernel(float* __restrict__ Z, i
       }
       Z[row * ld + j] = (cj > 0.f) ? yw * cj : qw;
     }
-    if (j < k) resid_part[(int64_t)blockIdx.x * k + j] = racc;
+    if (j < k) rp[grp * k + j] = racc;
+  }
+  __syncthreads();
+  for (int jj = tid; jj < k; jj += 256) {
+    float s = 0.f;
+    for (int g = 0; g < ngrp; ++g) s += rp[g * k + jj];
+    resid_part[(int64_t)blockIdx.x * k + jj] = s;
   }
 }
 
+// One wave per top-k column: lanes stride over the update blocks, shuffle-reduce
+// (fixed order, deterministic).
 __global__ __launch_bounds__(256) void rr_finish_kernel(const float* __restrict__ resid_part,
                                                         int nblk, int k,
                                                         const float* __restrict__ lam,
                                                         float* __restrict__ evals,
                                                         float* __restrict__ resid) {
-  __shared__ float mx[256];
-  const int tid = threadIdx.x;
+  __shared__ float mx[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float scale = fmaxf(fabsf(lam[0]), 1e-30f);
   float m = 0.f;
-  for (int j = tid; j < k; j += 256) {
+  for (int j = wave; j < k; j += 4) {
     float s = 0.f;
-    for (int b = 0; b < nblk; ++b) s += resid_part[(int64_t)b * k + j];
+    for (int b = lane; b < nblk; b += 64) s += resid_part[(int64_t)b * k + j];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
     const float rel = sqrtf(s) / scale;
-    resid[j] = rel;
-    evals[k - 1 - j] = lam[j];
+    if (lane == 0) {
+      resid[j] = rel;
+      evals[k - 1 - j] = lam[j];
+    }
     m = fmaxf(m, rel);
   }
-  mx[tid] = m;
+  if (lane == 0) mx[wave] = m;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o) mx[tid] = fmaxf(mx[tid], mx[tid + o]);
-    __syncthreads();
-  }
-  if (tid == 0) resid[k] = mx[0];
+  if (threadIdx.x == 0) resid[k] = fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3]));
 }
 
 size_t rr_small_shm(int p) {
-  return (size_t)(2 * p * p + 7 * p + RT / 64 + 8) * sizeof(float);
+  return (size_t)(2 * p * p + 6 * p + RT / 64 + 20) * sizeof(float);
 }
 
 }  // namespace
@@ -387,8 +454,8 @@ int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream) {
                                        (int)rr_small_shm(128)));
     attr = true;
   }
-  hipLaunchKernelGGL(rr_small_kernel, dim3(1), dim3(RT), shm, stream, b.C, p, b.Linv, b.Wtmp, b.W,
-                     b.lam, b.cs, b.info, 30);
+  hipLaunchKernelGGL(rr_small_kernel, dim3(1), dim3(RT), shm, stream, b.C, p, b.W, b.lam, b.cs,
+                     b.info, 30);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }
@@ -398,12 +465,13 @@ int rr_update_blocks(int64_t d) { return (int)cdiv(d, UR); }
 int rr_update_launch(const RRBuffers& b, int64_t d, int p, int k, float* V, int64_t ldv,
                      float* evals, hipStream_t stream) {
   const int nblk = rr_update_blocks(d);
-  const size_t shm = (size_t)(p * p + UR * 2 * p) * sizeof(float);
+  DEIG_REQUIRE(p >= 16 && p <= 128, "rr_update: p=%d out of range", p);
+  const size_t shm = (size_t)(p * p + UR * 2 * p + (256 / p) * k) * sizeof(float);
   static bool attr = false;
   if (!attr) {
     DEIG_HIP_CHECK(hipFuncSetAttribute((const void*)rr_update_kernel,
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)((128 * 128 + UR * 256) * sizeof(float))));
+                                       (int)((128 * 128 + UR * 256 + 16 * 128) * sizeof(float))));
     attr = true;
   }
   hipLaunchKernelGGL(rr_update_kernel, dim3(nblk), dim3(256), shm, stream, b.Z, d, p, k, b.W,

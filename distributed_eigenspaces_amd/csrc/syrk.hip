@@ -38,11 +38,17 @@ constexpr int BK = 32;           // rows of X per K-tile
 constexpr int NTHR = 512;        // 8 waves
 constexpr int PANEL = BK * BT;   // floats per panel buffer (32 KiB)
 constexpr int SLAB = BT * BT;    // floats per partial slab (256 KiB)
+// The MFMA accumulators are flushed into an fp32 slab every FLUSH_KT K-tiles
+// (4096 rows): a plain fp32 chain over all n rows would carry ~eps*sqrt(n/3)
+// relative error on the diagonal (5e-5 at n = 2^21); two-level summation keeps
+// it ~2e-6 and stays deterministic.
+constexpr int FLUSH_KT = 128;
 
 struct Sched {
   const float* X;
   float* S;
-  float* part;
+  float* part;   // 2 remainder slabs per block
+  float* accs;   // 1 flush slab per block (phase tiles)
   int64_t n, ldx, lds;
   int64_t NK;  // K-tiles per tile
   int64_t Wr;  // remainder work items (R * NK)
@@ -142,6 +148,44 @@ __device__ __forceinline__ void compute(const float* A, const float* B, f32x16 (
   }
 }
 
+__device__ __forceinline__ float* slab_ptr(float* slab, int wave, int mb, int nb, int g, int lane) {
+  return slab + ((((wave * 4 + mb) * 2 + nb) * 4 + g) * 64 + lane) * 4;
+}
+
+// acc (+ slab if !first) -> slab; acc = 0.  Register-order image, 16 B per lane.
+__device__ __forceinline__ void flush(float* slab, bool first, f32x16 (&acc)[4][2], int wave,
+                                      int lane) {
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4* ptr = reinterpret_cast<f32x4*>(slab_ptr(slab, wave, mb, nb, g, lane));
+        f32x4 v = {acc[mb][nb][4 * g], acc[mb][nb][4 * g + 1], acc[mb][nb][4 * g + 2],
+                   acc[mb][nb][4 * g + 3]};
+        if (!first) v += *ptr;
+        *ptr = v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[mb][nb][4 * g + e] = 0.f;
+      }
+}
+
+// acc += slab (the flushed part of this segment), before the epilogue.
+__device__ __forceinline__ void unflush(const float* slab, f32x16 (&acc)[4][2], int wave,
+                                        int lane) {
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(slab_ptr(const_cast<float*>(slab), wave, mb, nb, g, lane));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[mb][nb][4 * g + e] += v[e];
+      }
+}
+
 // One (tile, K-range) segment.  mode 0: direct store (full K); mode 1: partial slab.
 __device__ void segment(const Sched& s, float* lds, int tile, int64_t k0, int64_t k1, int slot,
                         bool partial) {
@@ -163,23 +207,31 @@ __device__ void segment(const Sched& s, float* lds, int tile, int64_t k0, int64_
       for (int r = 0; r < 16; ++r) acc[mb][nb][r] = 0.0f;
 
   // LDS: [buf][A|B][BK][BT]; buffer toggled by a scalar offset.
+  float* slab = partial ? s.part + (int64_t)slot * SLAB : s.accs + (int64_t)blockIdx.x * SLAB;
+  bool flushed = false;
   if (k0 < k1) {
     stage(s, k0, i0, j0, diag, lds, lds + PANEL, wave, lane16);
     kt_barrier();
     int cur = 0;
+    int since = 0;
     for (int64_t kt = k0; kt < k1; ++kt) {
       float* Ac = lds + cur * (2 * PANEL);
       float* An = lds + (cur ^ 1) * (2 * PANEL);
       if (kt + 1 < k1) stage(s, kt + 1, i0, j0, diag, An, An + PANEL, wave, lane16);
       compute(Ac, diag ? Ac : Ac + PANEL, acc, wi, wj, lane);
+      if (++since == FLUSH_KT && kt + 1 < k1) {
+        flush(slab, !flushed, acc, wave, lane);
+        flushed = true;
+        since = 0;
+      }
       kt_barrier();
       cur ^= 1;
     }
   }
+  if (flushed) unflush(slab, acc, wave, lane);
 
   const int c = lane & 31, h = lane >> 5;
   if (partial) {
-    float* slab = s.part + (int64_t)slot * SLAB;
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
@@ -312,10 +364,15 @@ void make_sched(Sched& s, int64_t n, int64_t d, int G) {
 
 }  // namespace
 
+// [G flush slabs][2G remainder slabs]
+static size_t ws_bytes_for(const Sched& s) {
+  return (size_t)(s.R > 0 ? 3 : 1) * s.G * SLAB * sizeof(float);
+}
+
 size_t syrk_workspace_bytes(int64_t n, int64_t d) {
   Sched s;
   make_sched(s, n, d, num_cus());
-  return s.R > 0 ? (size_t)2 * s.G * SLAB * sizeof(float) : 0;
+  return ws_bytes_for(s);
 }
 
 int syrk_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha, float* S,
@@ -335,10 +392,11 @@ int syrk_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha, 
   s.ldx = ldx;
   s.lds = lds;
   s.alpha = alpha;
-  const size_t need = s.R > 0 ? (size_t)2 * s.G * SLAB * sizeof(float) : 0;
-  if (ws_bytes < need || (need && !ws))
+  const size_t need = ws_bytes_for(s);
+  if (ws_bytes < need || !ws)
     return fail(DEIG_EWORKSPACE, "syrk: workspace %zu bytes < required %zu", ws_bytes, need);
-  s.part = static_cast<float*>(ws);
+  s.accs = static_cast<float*>(ws);
+  s.part = s.accs + (size_t)s.G * SLAB;
   hipLaunchKernelGGL(syrk_kernel, dim3(s.G), dim3(NTHR), 0, stream, s);
   DEIG_HIP_CHECK(hipGetLastError());
   if (s.R > 0) {

@@ -181,10 +181,14 @@ def test_syrk_full_width_phases_and_remainder(cuda):
     got = S[ii, jj].double()
     scale = S.diagonal().abs().max().double()
     assert float((got - ref).abs().max() / scale) < 2e-6
-    # linearity: alpha = 1 on two halves sums to the whole
+    # diagonal = longest positive sums: two-level (flushed) fp32 accumulation
+    dref = (X.double() ** 2).sum(0) / n
+    assert float(((S.diagonal().double() - dref).abs() / dref).max()) < 5e-6
+    # linearity: alpha = 1 on two halves sums to the whole (fp32 rounding of
+    # 2 x 20000-row sums vs one 40000-row sum)
     S1 = de.sigma_hat(X[: n // 2], alpha=1.0)
     S2 = de.sigma_hat(X[n // 2:], alpha=1.0)
-    assert float(((S1 + S2) / n - S).abs().max() / scale) < 2e-6
+    assert float(((S1 + S2) / n - S).abs().max() / scale) < 1e-5
 
 
 def test_full_size_worker_recovers_planted_subspace(cuda):
