@@ -50,6 +50,10 @@ SIGNATURES = {
     "deig_project_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, _fp, ctypes.c_int, _c_i64,
                                         _fp, _c_i64, _vp, _c_sz, _vp]),
     "deig_project_workspace": (_c_sz, [_c_i64, _c_i64, ctypes.c_int]),
+    "deig_gemm_skinny_f32": (ctypes.c_int, [ctypes.c_int, _fp, _c_i64, _fp, _c_i64, _fp, _c_i64,
+                                            _c_i64, _c_i64, _c_i64, ctypes.c_float,
+                                            ctypes.c_float, _vp, _c_sz, _vp]),
+    "deig_gemm_skinny_workspace": (_c_sz, [_c_i64, _c_i64, _c_i64]),
 }
 
 _lock = threading.Lock()

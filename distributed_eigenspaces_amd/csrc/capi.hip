@@ -268,4 +268,16 @@ int deig_project_f32(const float* X, int64_t n, int64_t d, int64_t ldx, const fl
   return project_launch(X, n, d, ldx, W, k, ldw, Y, ldy, ws, ws_bytes, (hipStream_t)stream);
 }
 
+size_t deig_gemm_skinny_workspace(int64_t M, int64_t N, int64_t K) {
+  return skinny_workspace_bytes(M, N, K);
+}
+
+int deig_gemm_skinny_f32(int trans_a, const float* A, int64_t lda, const float* B, int64_t ldb,
+                         float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha,
+                         float beta, void* ws, size_t ws_bytes, void* stream) {
+  g_err[0] = 0;
+  return skinny_launch(trans_a != 0, A, lda, B, ldb, C, ldc, M, N, K, alpha, beta,
+                       static_cast<float*>(ws), ws_bytes, (hipStream_t)stream);
+}
+
 }  // extern "C"

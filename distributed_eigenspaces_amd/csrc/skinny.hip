@@ -18,6 +18,8 @@
 // so the two 16-lane halves of a ds_read_b32 group hit disjoint banks.
 // Split-K over gridDim.y writes fp32 partial slabs; skinny_reduce_kernel sums
 // them in slice order (deterministic).
+#include <stdlib.h>
+
 #include "deig_internal.hpp"
 
 namespace deig {
@@ -214,11 +216,22 @@ int launch_t(int NB, const float* A, int64_t lda, const float* B, int64_t ldb, f
   }
 }
 
-// Split-K factor: enough blocks to fill the chip twice, >= 8 chunks per slice.
+// Split-K factor: enough blocks for ~4 resident per CU (latency hiding: HBM
+// latency under load is ~1-2 us, one chunk of MFMA work ~0.5 us), >= 8 chunks
+// per slice.  DEIG_SKINNY_BPC overrides the blocks-per-CU target (tuning).
+int blocks_per_cu() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DEIG_SKINNY_BPC");
+    v = (e && atoi(e) > 0) ? atoi(e) : 4;
+  }
+  return v;
+}
+
 int choose_ks(int64_t M, int64_t K) {
   const int64_t mb = cdiv(M, SBM);
   const int64_t nch = cdiv(K, SBK);
-  int64_t ks = cdiv(2 * (int64_t)num_cus(), mb);
+  int64_t ks = cdiv((int64_t)blocks_per_cu() * num_cus(), mb);
   const int64_t cap = nch / 8 > 1 ? nch / 8 : 1;
   if (ks > cap) ks = cap;
   if (ks < 1) ks = 1;

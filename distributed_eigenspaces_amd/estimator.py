@@ -49,9 +49,15 @@ def gather_bases(Wt_local: torch.Tensor, group=None) -> torch.Tensor:
     world = dist.get_world_size(group)
     if world == 1:
         return Wt_local
-    out = torch.empty((world * Wt_local.shape[0], Wt_local.shape[1]), dtype=Wt_local.dtype,
-                      device=Wt_local.device)
-    dist.all_gather_into_tensor(out, Wt_local.contiguous(), group=group)
+    src = Wt_local.contiguous()
+    if dist.get_backend(group) == "gloo" and src.is_cuda:
+        # rehearsal path (several ranks sharing one GPU): gloo gathers host tensors
+        host = src.cpu()
+        parts = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(parts, host, group=group)
+        return torch.cat(parts, dim=0).to(src.device)
+    out = torch.empty((world * src.shape[0], src.shape[1]), dtype=src.dtype, device=src.device)
+    dist.all_gather_into_tensor(out, src, group=group)
     return out
 
 

@@ -22,7 +22,7 @@ from . import _lib
 
 __all__ = [
     "sigma_hat", "topk_eigh", "projavg_topk", "oja_step", "default_subspace",
-    "EigResult", "require_device_tensor", "project", "stack_bases",
+    "EigResult", "require_device_tensor", "project", "stack_bases", "gemm_skinny",
 ]
 
 DEFAULT_TOL = 1e-6
@@ -317,3 +317,30 @@ def project(X: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
                                 _stream(X.device))
     _lib.check(rc, "deig_project_f32")
     return Y
+
+
+# ---------------------------------------------------------------- building block
+def gemm_skinny(A: torch.Tensor, B: torch.Tensor, trans_a: bool, alpha: float = 1.0,
+                beta: float = 0.0, C: torch.Tensor | None = None) -> torch.Tensor:
+    """C = alpha * op(A) @ B + beta * C on the solvers' skinny fp32-MFMA kernel.
+
+    trans_a: A is (K, M) and op(A) = A^T; else A is (M, K).  B is (K, N) with
+    N % 16 == 0 and N <= 256.  All row-major float32 on one device."""
+    A = require_device_tensor(A, "A")
+    B = require_device_tensor(B, "B")
+    K, M = (A.shape if trans_a else (A.shape[1], A.shape[0]))
+    N = B.shape[1]
+    if B.shape[0] != K:
+        raise ValueError("inner dimensions differ")
+    if C is None:
+        C = torch.zeros((M, N), dtype=torch.float32, device=A.device)
+    L = _lib.lib()
+    with torch.cuda.device(A.device):
+        nbytes = L.deig_gemm_skinny_workspace(M, N, K)
+        ws = _workspace(A.device, nbytes)
+        rc = L.deig_gemm_skinny_f32(int(trans_a), A.data_ptr(), A.stride(0), B.data_ptr(),
+                                    B.stride(0), C.data_ptr(), C.stride(0), M, N, K,
+                                    ctypes.c_float(alpha), ctypes.c_float(beta), ws.data_ptr(),
+                                    nbytes, _stream(A.device))
+    _lib.check(rc, "deig_gemm_skinny_f32")
+    return C

@@ -101,6 +101,16 @@ int deig_project_f32(const float* X, int64_t n, int64_t d, int64_t ldx, const fl
                      void* stream);
 size_t deig_project_workspace(int64_t n, int64_t d, int k);
 
+/* Building block of the solvers, exposed for direct testing / reuse:
+ * C[M x N] = alpha * op(A) * B + beta * C  on fp32 MFMA (16x16x4), N % 16 == 0, N <= 256.
+ * trans_a != 0: A is K x M row-major (lda), op(A) = A^T  (S*Q with S symmetric, Gram)
+ * trans_a == 0: A is M x K row-major (lda)              (Wt*Q, Xb*V)
+ * B is K x N row-major (ldb), C is M x N row-major (ldc).  Deterministic split-K. */
+int deig_gemm_skinny_f32(int trans_a, const float* A, int64_t lda, const float* B, int64_t ldb,
+                         float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha,
+                         float beta, void* ws, size_t ws_bytes, void* stream);
+size_t deig_gemm_skinny_workspace(int64_t M, int64_t N, int64_t K);
+
 #ifdef __cplusplus
 }
 #endif

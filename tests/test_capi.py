@@ -23,8 +23,9 @@ def test_version_and_error_string():
 
 def test_workspace_queries():
     L = _lib.lib()
-    # config-3 shard: d=8192 -> 528 tiles = 2 x 256 + 16 remainder tiles -> 2 slabs/CU
-    assert L.deig_syrk_workspace(1 << 21, 8192) == 2 * 256 * 256 * 256 * 4
+    # config-3 shard: d=8192 -> 528 tiles = 2 x 256 + 16 remainder tiles:
+    # one flush slab + two remainder slabs of 256 x 256 fp32 per CU
+    assert L.deig_syrk_workspace(1 << 21, 8192) == 3 * 256 * 256 * 256 * 4
     assert L.deig_syrk_workspace(1000, 256) > 0
     for d, k in [(64, 4), (3072, 16), (8192, 64), (16384, 128)]:
         p = L.deig_default_subspace(d, k)
