@@ -12,12 +12,18 @@ One step = time-to-eigenspace of the whole pipeline:
   server: top-k of the projector average (implicit operator) on rank 0.
 value = samples ingested per second over the whole job = N * n / t_step.
 
-Extra objects on the JSON line: ``roofline`` (SYRK vs fp32 MFMA peak, timed with
-HIP events on the launch stream), ``cpu_baseline`` (the float64 oracle on a
-bounded sample of the same workload, rank 0 at N = 1 only), ``breakdown`` and
-``accuracy`` (sin theta of the server basis vs the planted subspace).
+Extra objects on the JSON line: ``roofline`` (the covariance op vs the MFMA peak
+of the instructions it runs, timed with HIP events on the launch stream),
+``cpu_baseline`` (the float64 oracle on a bounded sample of the same workload,
+rank 0 at N = 1 only), ``breakdown`` and ``accuracy`` (sin theta of the server
+basis vs the planted subspace; Sigma_hat vs float64 on a sampled 16 x 16 block).
+
+Covariance algorithm (--syrk-algo, default auto = split3 at these sizes): fp32
+samples split into bf16 hi/lo pairs, 3 bf16 MFMA products per fp32 product,
+fp32 accumulation (include/deig.h); "fp32" = the f32 MFMA kernel.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2]
+       [--syrk-algo auto|split3|fp32]
        (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N)
 """
 from __future__ import annotations
@@ -37,6 +43,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 FP32_MFMA_PEAK = 157.3e12  # MI355X_MICROARCH.md: FP32 matrix, dense
+BF16_MFMA_PEAK = 2.5e15    # MI355X_MICROARCH.md: BF16 MFMA, dense (16 x the f32 rate)
 HBM_PEAK = 8.0e12
 
 CONFIGS = {
@@ -85,6 +92,7 @@ def main():
     ap.add_argument("--rows", type=int, default=0, help="override rows per GPU")
     ap.add_argument("--cpu-sample", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--syrk-algo", default="auto", choices=["auto", "split3", "fp32"])
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = rehearsal of the N>1 control flow with ranks sharing one GPU")
     args = ap.parse_args()
@@ -124,7 +132,7 @@ def main():
         e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         t0 = time.perf_counter()
         e[0].record(stream)
-        de.sigma_hat(X, out=S)
+        de.sigma_hat(X, out=S, algo=args.syrk_algo)
         e[1].record(stream)
         r = de.topk_eigh(S, k, check_finite=False)  # synchronises the stream
         t1 = time.perf_counter()
@@ -163,8 +171,27 @@ def main():
         elapsed = float(t.item())
 
     syrk_ms = float(np.mean([a.elapsed_time(b) for a, b in syrk_ev]))
-    flops = float(n) * d * (d + 1)
-    achieved = flops / (syrk_ms * 1e-3)
+    flops = float(n) * d * (d + 1)  # algorithmic: lower triangle incl. diagonal
+    algo = args.syrk_algo
+    if algo == "auto":
+        algo = "split3" if n >= 1024 else "fp32"
+    if algo == "split3":
+        # 3 bf16 MFMA products per fp32 product; peak = dense bf16 MFMA
+        mfma_flops, peak = 3.0 * flops, BF16_MFMA_PEAK
+        kernel = "covariance split3 (split_kernel + syrks_kernel + syrks_reduce_kernel + diag_corr_kernel)"
+        algorithmic = f"3 * n*d*(d+1) = {3 * flops:.4e} bf16 MFMA flop per launch (3 split products per fp32 product)"
+    else:
+        mfma_flops, peak = flops, FP32_MFMA_PEAK
+        kernel = "syrk_kernel (+ syrk_reduce_kernel)"
+        algorithmic = f"n*d*(d+1) = {flops:.4e} f32 MFMA flop per launch"
+    achieved = mfma_flops / (syrk_ms * 1e-3)
+    # Sigma_hat vs float64 on a sampled 16 x 16 block (all n rows)
+    cols = torch.randperm(d, generator=torch.Generator().manual_seed(7))[:16].to(dev)
+    Xs = X.index_select(1, cols).double()
+    S64 = (Xs.t() @ Xs) / n
+    Sblk = S.index_select(0, cols).index_select(1, cols).double()
+    sigma_err = float((Sblk - S64).abs().max() / S64.abs().max())
+    del Xs
 
     if rank == 0:
         sin_server = float(torch.linalg.svdvals(U.double().t() @ res.V.double()).min().clamp(max=1)
@@ -172,7 +199,7 @@ def main():
         sin_worker = float(torch.linalg.svdvals(U.double().t() @ r.V.double()).min().clamp(max=1)
                            .pow(2).neg().add(1).clamp(min=0).sqrt())
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", f"pmc_syrk_{args.config}.json")
+        pmc = os.path.join(ROOT, "profiles", f"pmc_syrk_{args.config}_{algo}.json")
         if os.path.exists(pmc) and not args.rows:
             try:
                 traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
@@ -198,11 +225,13 @@ def main():
             "config": {"workload": label, "rows_per_gpu": n, "total_rows": n * world, "d": d,
                        "k": k, "workers": m, "subspace_p": de.default_subspace(d, k),
                        "parallelism": f"dp{world} (one worker per GPU, RCCL all-gather)"},
-            "roofline": {"bound": "mfma", "kernel": "syrk_kernel", "achieved": achieved / 1e12,
-                         "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
-                         "frac": achieved / FP32_MFMA_PEAK, "traffic": traffic,
-                         "algorithmic": f"n*d*(d+1) = {flops:.4e} flop per launch",
-                         "launch_ms": syrk_ms},
+            "roofline": {"bound": "mfma", "kernel": kernel, "achieved": achieved / 1e12,
+                         "peak": peak / 1e12, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": traffic,
+                         "algorithmic": algorithmic, "launch_ms": syrk_ms,
+                         "fp32_equiv_tflops": flops / (syrk_ms * 1e-3) / 1e12,
+                         "fp32_mfma_peak": FP32_MFMA_PEAK / 1e12},
+            "syrk_algo": algo,
             "cpu_baseline": cpu,
             "breakdown": {"syrk_ms": syrk_ms,
                           "worker_eig_ms": 1e3 * float(np.mean(times["worker_eig"])) - syrk_ms,
@@ -212,7 +241,8 @@ def main():
                           "server_sweeps": res.sweeps},
             "accuracy": {"sin_theta_server_vs_planted": sin_server,
                          "sin_theta_worker0_vs_planted": sin_worker,
-                         "worker_resid": r.resid, "server_resid": res.resid},
+                         "worker_resid": r.resid, "server_resid": res.resid,
+                         "sigma_hat_rel_err_vs_f64_sampled": sigma_err},
         }
         print(json.dumps(line), flush=True)
     if world > 1:

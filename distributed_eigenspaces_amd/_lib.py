@@ -20,6 +20,10 @@ DEIG_NOT_CONVERGED = 1
 DEIG_EINVAL = -1
 DEIG_EHIP = -2
 DEIG_EWORKSPACE = -3
+DEIG_SYRK_AUTO = 0
+DEIG_SYRK_SPLIT3 = 1
+DEIG_SYRK_FP32 = 2
+SYRK_ALGOS = {"auto": DEIG_SYRK_AUTO, "split3": DEIG_SYRK_SPLIT3, "fp32": DEIG_SYRK_FP32}
 
 _c_i64 = ctypes.c_int64
 _c_sz = ctypes.c_size_t
@@ -32,6 +36,9 @@ SIGNATURES = {
     "deig_syrk_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, ctypes.c_float, _fp, _c_i64,
                                      _vp, _c_sz, _vp]),
     "deig_syrk_workspace": (_c_sz, [_c_i64, _c_i64]),
+    "deig_syrk_f32_ex": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, ctypes.c_float, _fp,
+                                        _c_i64, ctypes.c_int, _vp, _c_sz, _vp]),
+    "deig_syrk_workspace_ex": (_c_sz, [_c_i64, _c_i64, ctypes.c_int]),
     "deig_default_subspace": (ctypes.c_int, [_c_i64, ctypes.c_int]),
     "deig_topk_sym_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_float, _fp, ctypes.c_int, _c_i64,

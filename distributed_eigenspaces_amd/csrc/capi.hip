@@ -187,12 +187,36 @@ int deig_version(void) { return 0x000100; }
 
 const char* deig_last_error(void) { return g_err; }
 
-size_t deig_syrk_workspace(int64_t n, int64_t d) { return syrk_workspace_bytes(n, d); }
+static int syrk_resolve(int64_t n, int algo) {
+  if (algo != DEIG_SYRK_AUTO) return algo;
+  return n >= DEIG_SYRK_SPLIT_MIN_ROWS ? DEIG_SYRK_SPLIT3 : DEIG_SYRK_FP32;
+}
+
+size_t deig_syrk_workspace_ex(int64_t n, int64_t d, int algo) {
+  algo = syrk_resolve(n, algo);
+  if (algo == DEIG_SYRK_FP32) return syrk_workspace_bytes(n, d);
+  if (algo == DEIG_SYRK_SPLIT3) return syrk_split_workspace_bytes(n, d);
+  return 0;
+}
+
+int deig_syrk_f32_ex(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha, float* S,
+                     int64_t lds, int algo, void* ws, size_t ws_bytes, void* stream) {
+  g_err[0] = 0;
+  algo = syrk_resolve(n, algo);
+  if (algo == DEIG_SYRK_FP32)
+    return syrk_launch(X, n, d, ldx, alpha, S, lds, ws, ws_bytes, (hipStream_t)stream);
+  if (algo == DEIG_SYRK_SPLIT3)
+    return syrk_split_launch(X, n, d, ldx, alpha, S, lds, ws, ws_bytes, (hipStream_t)stream);
+  return fail(DEIG_EINVAL, "syrk: unknown algorithm %d", algo);
+}
+
+size_t deig_syrk_workspace(int64_t n, int64_t d) {
+  return deig_syrk_workspace_ex(n, d, DEIG_SYRK_DEFAULT);
+}
 
 int deig_syrk_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha, float* S,
                   int64_t lds, void* ws, size_t ws_bytes, void* stream) {
-  g_err[0] = 0;
-  return syrk_launch(X, n, d, ldx, alpha, S, lds, ws, ws_bytes, (hipStream_t)stream);
+  return deig_syrk_f32_ex(X, n, d, ldx, alpha, S, lds, DEIG_SYRK_DEFAULT, ws, ws_bytes, stream);
 }
 
 int deig_default_subspace(int64_t d, int k) {

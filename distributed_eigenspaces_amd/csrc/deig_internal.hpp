@@ -59,6 +59,10 @@ struct Carve {
 size_t syrk_workspace_bytes(int64_t n, int64_t d);
 int syrk_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha, float* S,
                 int64_t lds, void* ws, size_t ws_bytes, hipStream_t stream);
+// Split-bf16 covariance SYRK (syrk_split.hip).
+size_t syrk_split_workspace_bytes(int64_t n, int64_t d);
+int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha, float* S,
+                      int64_t lds, void* ws, size_t ws_bytes, hipStream_t stream);
 
 // Skinny GEMM (skinny.hip):  C[M x N] = alpha * op(A) * B + beta * C
 //   trans_a = true : A is K x M row-major (op(A) = A^T)

@@ -1,0 +1,529 @@
+// Covariance SYRK on CDNA4 bf16 MFMA with split fp32 operands ("split3"):
+//   S = alpha * X^T X  (+ S if accumulating),  X: n x d fp32 row-major.
+//
+// Replaces SlaveNode.compute_sigma_hat_ (distributed.py:59-70; np.dot(x.T, x)
+// on a transposed view -> OpenBLAS dsyrk, then /= n).  gfx950 has no xf32 MFMA
+// and its f32 MFMA runs at 1/16 of the bf16 rate, so every fp32 sample is split
+// once into x = hi + lo (hi = bf16(x), lo = bf16(x - hi); |x - hi - lo| <=
+// 2^-17 |x|) and each product is formed from three bf16 MFMA products
+//   x_a x_b ~ hi_a hi_b + hi_a lo_b + lo_a hi_b
+// accumulated in fp32 (the bf16 products are exact in fp32).  The dropped
+// lo_a lo_b term is ~2^-18 |x_a x_b|: negligible off the diagonal (zero-mean
+// rounding residues), but it biases the diagonal by ~-3e-6 relative, so the
+// split pass also accumulates sum_k lo_ik^2 per feature and a last kernel adds it
+// to S[i][i].  Net error vs float64 ~1e-7 * max|S|, the same order as the
+// fp32-MFMA kernel (syrk.hip), at 16/3 x its MFMA rate.
+//
+// Pipeline per row chunk (bounded workspace; chunks accumulate into S):
+//   split_kernel   X (fp32, HBM) -> XP: bf16 hi/lo image in MFMA operand order,
+//                  [octet of 8 rows][hi|lo][feature (padded to 256)][8 rows],
+//                  rows padded with zeros to a multiple of 32, + lo^2 partials;
+//   syrks_kernel   persistent, one 512-thread block per CU, 256 x 256 lower
+//                  tiles, v_mfma_f32_32x32x16_bf16, K-tile = 32 rows whose two
+//                  panels (32 KiB each: 4 octets x {hi, lo} x 256 features x 16 B)
+//                  are DMA'd HBM -> LDS with buffer_load ... lds, double-buffered
+//                  (128 KiB); conflict-free ds_read_b128 operand reads;
+//   syrks_reduce   split-K remainder tiles, summed in block order (deterministic);
+//   diag_corr      S[i][i] += alpha * sum lo_i^2.
+// Tile order: 4 x 8 super-tiles of the lower triangle, so the ~32 tiles an XCD
+// runs concurrently share few panels in its L2.  Work decomposition (phases +
+// K-split remainder, no atomics) is the one of syrk.hip.
+#include "deig_internal.hpp"
+
+namespace deig {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BT = 256;                      // tile edge (features)
+constexpr int BK = 32;                       // rows per K-tile
+constexpr int NTHR = 512;                    // 8 waves: 2 (i) x 4 (j), wave tile 128 x 64
+constexpr int SLICE_B = BT * 16;             // (octet, hi|lo) slice of a panel: 4 KiB
+constexpr int PANEL_B = (BK / 8) * 2 * SLICE_B;  // 32 KiB
+constexpr int BUF_B = 2 * PANEL_B;           // panels A | B: 64 KiB
+constexpr int SLAB = BT * BT;                // floats per partial slab
+constexpr int FLUSH_KT = 128;                // two-level fp32 summation every 4096 rows
+constexpr int SPLIT_YB = 256;                // row groups of the split pass
+constexpr int SUPER_H = 4, SUPER_W = 8;      // super-tile shape (tiles)
+// Recommended XP image per chunk: a config-3 shard (2^21 x 8192) in one chunk on
+// a 288 GB MI355X; callers with less room pass a smaller workspace and get chunks.
+constexpr size_t DEFAULT_CHUNK_BYTES = size_t(64) << 30;
+
+struct SSched {
+  const unsigned char* XP;  // bf16 image of this chunk
+  float* S;
+  float* part;   // 2 remainder slabs per block
+  float* accs;   // 1 flush slab per block
+  const int* order;  // tile order: ti | tj << 16
+  int64_t lds, dp;
+  int64_t NK;  // K-tiles in the chunk
+  int64_t Wr;  // remainder work items (R * NK)
+  int d, nt, T, G, q, R;
+  float alpha;
+  int beta;
+};
+
+__device__ __forceinline__ int xcd_logical(int b, int G) {
+  const int x = b & 7, qq = G >> 3, rr = G & 7;
+  const int base = (x < rr) ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq;
+  return base + (b >> 3);
+}
+
+__device__ __forceinline__ int64_t block_of(int64_t pos, int64_t Wr, int G) {
+  return ((pos + 1) * (int64_t)G + Wr - 1) / Wr - 1;
+}
+
+__device__ __forceinline__ i32x4 make_rsrc(const void* base, uint32_t nrec) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  i32x4 r;
+  r[0] = (int)(uint32_t)a;
+  r[1] = (int)((uint32_t)(a >> 32) & 0xffffu);
+  r[2] = (int)nrec;
+  r[3] = 0x00020000;
+  return r;
+}
+
+// 16 B per lane HBM -> LDS at m0 + 16 * lane (see syrk.hip for why inline asm).
+__device__ __forceinline__ void dma16(i32x4 rsrc, int voff, const void* lds_dst) {
+  const unsigned m0v = (unsigned)(uintptr_t)(lds_void*)lds_dst;
+  asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               :
+               : "v"(voff), "s"(rsrc), "s"(m0v)
+               : "memory", "m0");
+}
+
+__device__ __forceinline__ void kt_barrier() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// K-tile kt of panels i0 (-> A) and j0 (-> B).  Wave w moves slice w = (octet
+// w/2, hi|lo w%2) of each panel: 4 KiB = four 1-KiB wave-instructions.
+__device__ __forceinline__ void stage(const SSched& s, int64_t kt, int i0, int j0, bool diag,
+                                     unsigned char* buf, int wave, int lane16) {
+  const i32x4 rsrc = make_rsrc(s.XP + kt * (int64_t)(BK / 8) * 2 * s.dp * 16,
+                               (uint32_t)((BK / 8) * 2 * s.dp * 16));
+  int l16 = lane16;
+  asm volatile("" : "+v"(l16));
+  const int sl = (int)(wave * s.dp) * 16;  // slice base in the K-tile image
+  unsigned char* dA = buf + wave * SLICE_B;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) dma16(rsrc, l16 + sl + i0 * 16 + p * 1024, dA + p * 1024);
+  if (!diag) {
+    unsigned char* dB = buf + PANEL_B + wave * SLICE_B;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) dma16(rsrc, l16 + sl + j0 * 16 + p * 1024, dB + p * 1024);
+  }
+}
+
+__device__ __forceinline__ void compute(const unsigned char* A, const unsigned char* B,
+                                        f32x16 (&acc)[4][2], int wi, int wj, int lane) {
+  const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int st = 0; st < BK / 16; ++st) {
+    const int o = 2 * st + h;  // octet this lane's 8 k-values come from
+    const unsigned char* ph = A + ((o * 2) * BT + 128 * wi + c) * 16;
+    const unsigned char* qh = B + ((o * 2) * BT + 64 * wj + c) * 16;
+    bf16x8 ahi[4], alo[4], bhi[2], blo[2];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      ahi[mb] = *reinterpret_cast<const bf16x8*>(ph + (32 * mb) * 16);
+      alo[mb] = *reinterpret_cast<const bf16x8*>(ph + (BT + 32 * mb) * 16);
+    }
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      bhi[nb] = *reinterpret_cast<const bf16x8*>(qh + (32 * nb) * 16);
+      blo[nb] = *reinterpret_cast<const bf16x8*>(qh + (BT + 32 * nb) * 16);
+    }
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[mb], bhi[nb], acc[mb][nb], 0, 0, 0);
+        acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[mb], blo[nb], acc[mb][nb], 0, 0, 0);
+        acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[mb], bhi[nb], acc[mb][nb], 0, 0, 0);
+      }
+  }
+}
+
+__device__ __forceinline__ f32x4* slab_at(float* slab, int wave, int mb, int nb, int g, int lane) {
+  return reinterpret_cast<f32x4*>(slab + ((((wave * 4 + mb) * 2 + nb) * 4 + g) * 64 + lane) * 4);
+}
+
+__device__ __forceinline__ void flush(float* slab, bool first, f32x16 (&acc)[4][2], int wave,
+                                      int lane) {
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4* ptr = slab_at(slab, wave, mb, nb, g, lane);
+        f32x4 v = {acc[mb][nb][4 * g], acc[mb][nb][4 * g + 1], acc[mb][nb][4 * g + 2],
+                   acc[mb][nb][4 * g + 3]};
+        if (!first) v += *ptr;
+        *ptr = v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[mb][nb][4 * g + e] = 0.f;
+      }
+}
+
+__device__ __forceinline__ void unflush(float* slab, f32x16 (&acc)[4][2], int wave, int lane) {
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 v = *slab_at(slab, wave, mb, nb, g, lane);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[mb][nb][4 * g + e] += v[e];
+      }
+}
+
+// Store 4 consecutive rows ib..ib+3 of column j (values = alpha * a[u] (+ S)),
+// into S[i][j] and the mirror S[j][i].  Diagonal tiles keep only i >= j, so both
+// triangles come from the same register (bit-exact symmetry).
+__device__ __forceinline__ void store4(const SSched& s, int ib, int j, bool diag, const float* a) {
+  if (ib >= s.d || j >= s.d) return;
+  float v[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    float* p = s.S + (int64_t)(ib + u) * s.lds + j;
+    v[u] = s.alpha * a[u];
+    if (s.beta && (!diag || ib + u >= j)) v[u] += *p;
+  }
+  if (!diag) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s.S[(int64_t)(ib + u) * s.lds + j] = v[u];
+    const f32x4 w = {v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f32x4*>(s.S + (int64_t)j * s.lds + ib) = w;
+  } else {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (ib + u >= j) {
+        s.S[(int64_t)(ib + u) * s.lds + j] = v[u];
+        s.S[(int64_t)j * s.lds + ib + u] = v[u];
+      }
+  }
+}
+
+__device__ void segment(const SSched& s, unsigned char* lds, int tile, int64_t k0, int64_t k1,
+                        int slot, bool partial) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wi = wave >> 2, wj = wave & 3;
+  const int lane16 = lane * 16;
+  const int tt = s.order[tile];
+  const int ti = tt & 0xffff, tj = tt >> 16;
+  const int i0 = ti * BT, j0 = tj * BT;
+  const bool diag = (ti == tj);
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mb][nb][r] = 0.0f;
+
+  float* slab = partial ? s.part + (int64_t)slot * SLAB : s.accs + (int64_t)blockIdx.x * SLAB;
+  bool flushed = false;
+  if (k0 < k1) {
+    stage(s, k0, i0, j0, diag, lds, wave, lane16);
+    kt_barrier();
+    int cur = 0, since = 0;
+    for (int64_t kt = k0; kt < k1; ++kt) {
+      unsigned char* bc = lds + cur * BUF_B;
+      unsigned char* bn = lds + (cur ^ 1) * BUF_B;
+      if (kt + 1 < k1) stage(s, kt + 1, i0, j0, diag, bn, wave, lane16);
+      compute(bc, diag ? bc : bc + PANEL_B, acc, wi, wj, lane);
+      if (++since == FLUSH_KT && kt + 1 < k1) {
+        flush(slab, !flushed, acc, wave, lane);
+        flushed = true;
+        since = 0;
+      }
+      kt_barrier();
+      cur ^= 1;
+    }
+  }
+  if (flushed) unflush(slab, acc, wave, lane);
+
+  if (partial) {
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4 v = {acc[mb][nb][4 * g], acc[mb][nb][4 * g + 1], acc[mb][nb][4 * g + 2],
+                     acc[mb][nb][4 * g + 3]};
+          *slab_at(slab, wave, mb, nb, g, lane) = v;
+        }
+    return;
+  }
+  const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float a[4] = {acc[mb][nb][4 * g], acc[mb][nb][4 * g + 1], acc[mb][nb][4 * g + 2],
+                            acc[mb][nb][4 * g + 3]};
+        store4(s, i0 + 128 * wi + 32 * mb + 8 * g + 4 * h, j0 + 64 * wj + 32 * nb + c, diag, a);
+      }
+}
+
+__global__ __launch_bounds__(NTHR) void syrks_kernel(SSched s) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * BUF_B];
+  const int b = blockIdx.x;
+  const int L = xcd_logical(b, s.G);
+  int64_t pos = 0, end = 0;
+  if (s.R > 0) {
+    pos = (int64_t)b * s.Wr / s.G;
+    end = (int64_t)(b + 1) * s.Wr / s.G;
+  }
+  int m = 0, seg = 0;
+  for (;;) {
+    int tile, slot = 0;
+    int64_t k0, k1;
+    bool partial;
+    if (m < s.q) {
+      tile = m * s.G + L;
+      k0 = 0;
+      k1 = s.NK;
+      partial = false;
+      ++m;
+    } else if (pos < end) {
+      const int64_t r = pos / s.NK;
+      k0 = pos - r * s.NK;
+      k1 = k0 + (end - pos);
+      if (k1 > s.NK) k1 = s.NK;
+      tile = s.q * s.G + (int)r;
+      slot = 2 * b + seg;
+      partial = true;
+      pos += k1 - k0;
+      ++seg;
+    } else {
+      break;
+    }
+    segment(s, lds, tile, k0, k1, slot, partial);
+  }
+}
+
+// grid (R, SLAB/4/256): one thread per float4 of a remainder tile's slab image.
+__global__ __launch_bounds__(256) void syrks_reduce_kernel(SSched s) {
+  const int r = blockIdx.x;
+  const int f = blockIdx.y * 256 + threadIdx.x;
+  const int lane = f & 63, g = (f >> 6) & 3, nb = (f >> 8) & 1, mb = (f >> 9) & 3, wave = f >> 11;
+  const int wi = wave >> 2, wj = wave & 3, c = lane & 31, h = lane >> 5;
+  const int tt = s.order[s.q * s.G + r];
+  const int ti = tt & 0xffff, tj = tt >> 16;
+  const bool diag = (ti == tj);
+  const int64_t pos0 = (int64_t)r * s.NK, pos1 = pos0 + s.NK;
+  const int64_t bf = block_of(pos0, s.Wr, s.G), bl = block_of(pos1 - 1, s.Wr, s.G);
+  f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t b = bf; b <= bl; ++b) {
+    const int64_t sb = b * s.Wr / s.G, eb = (b + 1) * s.Wr / s.G;
+    if (eb <= sb || eb <= pos0 || sb >= pos1) continue;
+    const int64_t slot = 2 * b + (sb < pos0 ? 1 : 0);
+    sum += *reinterpret_cast<const f32x4*>(s.part + slot * SLAB + (int64_t)f * 4);
+  }
+  const float a[4] = {sum[0], sum[1], sum[2], sum[3]};
+  store4(s, ti * BT + 128 * wi + 32 * mb + 8 * g + 4 * h, tj * BT + 64 * wj + 32 * nb + c, diag, a);
+}
+
+__device__ __forceinline__ uint32_t bf16_rne(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+// X rows [0, n) of the chunk -> XP (noct octets; rows >= n and features >= d
+// are zeros) + per-block partial sums of lo^2 per feature (corr[blockIdx.y][f]).
+// grid (dp / 256, YB), 256 threads; lane handles features fb + lane + 64 q.
+__global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ X, int64_t n,
+                                                    int64_t ldx, int d, int64_t dp, int64_t noct,
+                                                    unsigned char* __restrict__ XP,
+                                                    float* __restrict__ corr) {
+  __shared__ float red[4][256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t fb = (int64_t)blockIdx.x * 256;
+  float sq[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t o = (int64_t)blockIdx.y * 4 + w; o < noct; o += (int64_t)gridDim.y * 4) {
+    float v[4][8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int64_t row = o * 8 + r;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t f = fb + lane + 64 * q;
+        v[q][r] = (row < n && f < d) ? __builtin_nontemporal_load(X + row * ldx + f) : 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      u32x4 hv, lv;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const uint32_t h0 = bf16_rne(v[q][2 * p]), h1 = bf16_rne(v[q][2 * p + 1]);
+        const float r0 = v[q][2 * p] - __uint_as_float(h0 << 16);
+        const float r1 = v[q][2 * p + 1] - __uint_as_float(h1 << 16);
+        const uint32_t l0 = bf16_rne(r0), l1 = bf16_rne(r1);
+        const float lf0 = __uint_as_float(l0 << 16), lf1 = __uint_as_float(l1 << 16);
+        sq[q] += lf0 * lf0 + lf1 * lf1;
+        hv[p] = h0 | (h1 << 16);
+        lv[p] = l0 | (l1 << 16);
+      }
+      const int64_t f = fb + lane + 64 * q;
+      *reinterpret_cast<u32x4*>(XP + ((o * 2 + 0) * dp + f) * 16) = hv;
+      *reinterpret_cast<u32x4*>(XP + ((o * 2 + 1) * dp + f) * 16) = lv;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[w][lane + 64 * q] = sq[q];
+  __syncthreads();
+  const int t = threadIdx.x;
+  corr[(int64_t)blockIdx.y * dp + fb + t] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+}
+
+// S[i][i] += alpha * sum_y corr[y][i]  (the dropped lo * lo term on the diagonal).
+__global__ __launch_bounds__(256) void diag_corr_kernel(const float* __restrict__ corr, int yb,
+                                                        int64_t dp, int d, float alpha, float* S,
+                                                        int64_t lds) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= d) return;
+  float c = 0.f;
+  for (int y = 0; y < yb; ++y) c += corr[(int64_t)y * dp + i];
+  S[(int64_t)i * lds + i] += alpha * c;
+}
+
+// Lower-triangle tiles in super-tile order (SUPER_H tile rows x SUPER_W tile cols).
+__global__ void tile_order_kernel(int nt, int* order) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int idx = 0;
+  for (int R0 = 0; R0 < nt; R0 += SUPER_H) {
+    const int rmax = R0 + SUPER_H < nt ? R0 + SUPER_H : nt;
+    for (int C0 = 0; C0 < rmax; C0 += SUPER_W)
+      for (int ti = R0; ti < rmax; ++ti)
+        for (int tj = C0; tj < C0 + SUPER_W && tj <= ti; ++tj) order[idx++] = ti | (tj << 16);
+  }
+}
+
+struct Layout {
+  int64_t dp, nt, T, G, q, R, yb_max, chunk_rows;
+  size_t off_order, off_accs, off_part, off_corr, off_xp, total;
+};
+
+// Workspace: [order][G flush slabs][2G remainder slabs][corr YB x dp][XP chunk].
+Layout make_layout(int64_t n, int64_t d, int G, int64_t chunk_rows) {
+  Layout L;
+  L.dp = cdiv(d, BT) * BT;
+  L.nt = L.dp / BT;
+  L.T = L.nt * (L.nt + 1) / 2;
+  L.G = G;
+  L.q = L.T / G;
+  L.R = L.T % G;
+  L.yb_max = SPLIT_YB;
+  L.chunk_rows = chunk_rows;
+  size_t off = 0;
+  L.off_order = off;
+  off = align_up(off + sizeof(int) * L.T, 256);
+  L.off_accs = off;
+  off += sizeof(float) * (size_t)G * SLAB;
+  L.off_part = off;
+  if (L.R > 0) off += sizeof(float) * (size_t)2 * G * SLAB;
+  L.off_corr = off;
+  off = align_up(off + sizeof(float) * (size_t)L.yb_max * L.dp, 256);
+  L.off_xp = off;
+  off += (size_t)chunk_rows * L.dp * 4;
+  L.total = off;
+  (void)n;
+  return L;
+}
+
+int64_t default_chunk_rows(int64_t n, int64_t d) {
+  const int64_t dp = cdiv(d, BT) * BT;
+  const int64_t n32 = cdiv(n, BK) * BK;
+  int64_t cap = (int64_t)(DEFAULT_CHUNK_BYTES / (size_t)(dp * 4)) / BK * BK;
+  if (cap < BK) cap = BK;
+  return n32 < cap ? n32 : cap;
+}
+
+}  // namespace
+
+size_t syrk_split_workspace_bytes(int64_t n, int64_t d) {
+  if (n < 1 || d < 1) return 0;
+  return make_layout(n, d, num_cus(), default_chunk_rows(n, d)).total;
+}
+
+int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha, float* S,
+                      int64_t lds, void* ws, size_t ws_bytes, hipStream_t stream) {
+  DEIG_REQUIRE(n >= 1, "syrk: n must be >= 1 (got %lld)", (long long)n);
+  DEIG_REQUIRE(d >= 1 && d % 4 == 0, "syrk: d must be a positive multiple of 4 (got %lld)",
+               (long long)d);
+  DEIG_REQUIRE(d <= (1 << 16) - BT, "syrk: d too large (%lld)", (long long)d);
+  DEIG_REQUIRE(ldx >= d && ldx % 4 == 0, "syrk: ldx must be >= d and a multiple of 4");
+  DEIG_REQUIRE(lds >= d && lds % 4 == 0, "syrk: lds must be >= d and a multiple of 4");
+  DEIG_REQUIRE(X && S && aligned16(X) && aligned16(S), "syrk: X and S must be 16-byte aligned");
+  const int G = num_cus();
+  // Largest chunk (multiple of 32 rows, <= n rounded up) that fits the workspace.
+  Layout L0 = make_layout(n, d, G, 0);
+  if (!ws || ws_bytes < L0.total + (size_t)BK * L0.dp * 4)
+    return fail(DEIG_EWORKSPACE, "syrk: workspace %zu bytes < minimum %zu", ws_bytes,
+                L0.total + (size_t)BK * L0.dp * 4);
+  int64_t chunk = (int64_t)((ws_bytes - L0.total) / (size_t)(L0.dp * 4)) / BK * BK;
+  const int64_t n32 = cdiv(n, BK) * BK;
+  if (chunk > n32) chunk = n32;
+  const Layout L = make_layout(n, d, G, chunk);
+  char* base = static_cast<char*>(ws);
+
+  SSched s;
+  s.S = S;
+  s.lds = lds;
+  s.dp = L.dp;
+  s.d = (int)d;
+  s.nt = (int)L.nt;
+  s.T = (int)L.T;
+  s.G = G;
+  s.q = (int)L.q;
+  s.R = (int)L.R;
+  s.alpha = alpha;
+  s.order = reinterpret_cast<const int*>(base + L.off_order);
+  s.accs = reinterpret_cast<float*>(base + L.off_accs);
+  s.part = reinterpret_cast<float*>(base + L.off_part);
+  s.XP = reinterpret_cast<const unsigned char*>(base + L.off_xp);
+  float* corr = reinterpret_cast<float*>(base + L.off_corr);
+  unsigned char* xp = reinterpret_cast<unsigned char*>(base + L.off_xp);
+
+  hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(64), 0, stream, s.nt,
+                     reinterpret_cast<int*>(base + L.off_order));
+  DEIG_HIP_CHECK(hipGetLastError());
+  for (int64_t r0 = 0, c = 0; r0 < n; r0 += chunk, ++c) {
+    const int64_t rows = (n - r0) < chunk ? (n - r0) : chunk;
+    const int64_t nk = cdiv(rows, BK);
+    const int64_t noct = nk * (BK / 8);
+    int64_t yb = cdiv(noct, 4);
+    if (yb > L.yb_max) yb = L.yb_max;
+    hipLaunchKernelGGL(split_kernel, dim3((unsigned)(L.dp / 256), (unsigned)yb), dim3(256), 0,
+                       stream, X + r0 * ldx, rows, ldx, (int)d, L.dp, noct, xp, corr);
+    DEIG_HIP_CHECK(hipGetLastError());
+    s.NK = nk;
+    s.Wr = (int64_t)s.R * nk;
+    s.beta = c > 0 ? 1 : 0;
+    hipLaunchKernelGGL(syrks_kernel, dim3(G), dim3(NTHR), 0, stream, s);
+    DEIG_HIP_CHECK(hipGetLastError());
+    if (s.R > 0) {
+      hipLaunchKernelGGL(syrks_reduce_kernel, dim3(s.R, SLAB / 4 / 256), dim3(256), 0, stream, s);
+      DEIG_HIP_CHECK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(diag_corr_kernel, dim3((unsigned)cdiv(d, 256)), dim3(256), 0, stream, corr,
+                       (int)yb, L.dp, (int)d, alpha, S, lds);
+    DEIG_HIP_CHECK(hipGetLastError());
+  }
+  return DEIG_OK;
+}
+
+}  // namespace deig

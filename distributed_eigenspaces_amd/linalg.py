@@ -99,13 +99,19 @@ def default_subspace(d: int, k: int) -> int:
 
 # ---------------------------------------------------------------- covariance
 def sigma_hat(x: torch.Tensor, alpha: float | None = None,
-              out: torch.Tensor | None = None) -> torch.Tensor:
+              out: torch.Tensor | None = None, algo: str = "auto") -> torch.Tensor:
     """Sigma_hat = alpha * X^T X with alpha = 1/n by default (uncentered).
 
     GPU replacement for ``SlaveNode.compute_sigma_hat_`` (distributed.py:59-70).
     x: (n, d) float32 on the GPU.  Returns a (d, d) float32 tensor, bit-exactly
     symmetric.  Columns are zero-padded to a multiple of 4 internally if needed.
+    algo: "split3" (fp32 operands as bf16 hi/lo pairs on bf16 MFMA, fp32
+    accumulation, see include/deig.h), "fp32" (f32 MFMA fma chain) or "auto"
+    (default: split3 for n >= 1024 rows, fp32 below).
     """
+    if algo not in _lib.SYRK_ALGOS:
+        raise ValueError(f"algo must be one of {sorted(_lib.SYRK_ALGOS)}, got {algo!r}")
+    code = _lib.SYRK_ALGOS[algo]
     x = require_device_tensor(x, "sigma_hat")
     if x.dim() != 2:
         raise ValueError(f"x must be 2-D (n, d), got {tuple(x.shape)}")
@@ -123,12 +129,13 @@ def sigma_hat(x: torch.Tensor, alpha: float | None = None,
         S = torch.empty((dp, dp), dtype=torch.float32, device=x.device)
     L = _lib.lib()
     with torch.cuda.device(x.device):
-        nbytes = L.deig_syrk_workspace(n, dp)
+        nbytes = L.deig_syrk_workspace_ex(n, dp, code)
         ws = _workspace(x.device, nbytes) if nbytes else None
-        rc = L.deig_syrk_f32(xx.data_ptr(), n, dp, xx.stride(0), ctypes.c_float(a), S.data_ptr(),
-                             S.stride(0), ws.data_ptr() if ws is not None else None,
-                             nbytes, _stream(x.device))
-    _lib.check(rc, "deig_syrk_f32")
+        rc = L.deig_syrk_f32_ex(xx.data_ptr(), n, dp, xx.stride(0), ctypes.c_float(a),
+                                S.data_ptr(), S.stride(0), code,
+                                ws.data_ptr() if ws is not None else None, nbytes,
+                                _stream(x.device))
+    _lib.check(rc, "deig_syrk_f32_ex")
     if dp != d:
         S = S[:d, :d].contiguous()
         if out is not None:

@@ -41,14 +41,35 @@ int deig_version(void);
 /* Thread-local message for the last nonzero return on this thread ("" if none). */
 const char* deig_last_error(void);
 
+/* Covariance algorithms (deig_syrk_f32_ex):
+ *  DEIG_SYRK_SPLIT3: each fp32 sample split once into bf16 hi + lo; products
+ *    from 3 bf16 MFMAs (hi*hi + hi*lo + lo*hi), fp32 accumulation, the dropped
+ *    lo*lo term restored exactly on the diagonal.  Per-product error <= ~3*2^-16
+ *    relative, zero-mean, so it averages out over rows: max |S - S_f64| / max|S|
+ *    ~1e-6 at n = 512, ~2e-7 at n >= 32k (fp32 kernel: ~1e-7..2e-6), at 16/3 x
+ *    the f32 MFMA rate.
+ *  DEIG_SYRK_FP32: v_mfma_f32_32x32x2_f32 (exact fp32 fma chain).
+ *  DEIG_SYRK_AUTO (default): SPLIT3 for n >= DEIG_SYRK_SPLIT_MIN_ROWS, else FP32. */
+#define DEIG_SYRK_AUTO 0
+#define DEIG_SYRK_SPLIT3 1
+#define DEIG_SYRK_FP32 2
+#define DEIG_SYRK_DEFAULT DEIG_SYRK_AUTO
+#define DEIG_SYRK_SPLIT_MIN_ROWS 1024
+
 /* Sigma_hat = alpha * X^T X  (alpha = 1/n reproduces the reference).
  * Replaces SlaveNode.compute_sigma_hat_  distributed.py:59-70
  * (np.zeros((d,d)) += np.dot(x.T, x); /= n  ->  OpenBLAS dsyrk).
- * fp32 in, fp32 MFMA accumulate; output is bit-exactly symmetric.
- * Requires n >= 1, d % 4 == 0, ldx % 4 == 0, lds % 4 == 0, 16-byte aligned X, S. */
+ * fp32 in, fp32 accumulate (DEIG_SYRK_DEFAULT); output is bit-exactly symmetric.
+ * Requires n >= 1, d % 4 == 0, ldx % 4 == 0, lds % 4 == 0, 16-byte aligned X, S.
+ * The workspace query returns the recommended size; SPLIT3 works on row chunks
+ * that fit the workspace given (more workspace -> fewer, larger chunks). */
 int deig_syrk_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha,
                   float* S, int64_t lds, void* ws, size_t ws_bytes, void* stream);
 size_t deig_syrk_workspace(int64_t n, int64_t d);
+/* Same with an explicit algorithm (DEIG_SYRK_*). */
+int deig_syrk_f32_ex(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha,
+                     float* S, int64_t lds, int algo, void* ws, size_t ws_bytes, void* stream);
+size_t deig_syrk_workspace_ex(int64_t n, int64_t d, int algo);
 
 /* Subspace size the solvers use for a given k when the caller passes p <= 0. */
 int deig_default_subspace(int64_t d, int k);

@@ -25,7 +25,15 @@ def test_workspace_queries():
     L = _lib.lib()
     # config-3 shard: d=8192 -> 528 tiles = 2 x 256 + 16 remainder tiles:
     # one flush slab + two remainder slabs of 256 x 256 fp32 per CU
-    assert L.deig_syrk_workspace(1 << 21, 8192) == 3 * 256 * 256 * 256 * 4
+    n, d = 1 << 21, 8192
+    slabs = 3 * 256 * 256 * 256 * 4
+    assert L.deig_syrk_workspace_ex(n, d, _lib.DEIG_SYRK_FP32) == slabs
+    # split3 adds the bf16 hi/lo image of the shard (4 B per sample value, one chunk)
+    ws = L.deig_syrk_workspace_ex(n, d, _lib.DEIG_SYRK_SPLIT3)
+    assert n * d * 4 + slabs <= ws <= n * d * 4 + slabs + (16 << 20)
+    assert L.deig_syrk_workspace(n, d) == ws  # default = auto = split3 at n >= 1024
+    assert L.deig_syrk_workspace(1000, 256) == L.deig_syrk_workspace_ex(1000, 256,
+                                                                        _lib.DEIG_SYRK_FP32)
     assert L.deig_syrk_workspace(1000, 256) > 0
     for d, k in [(64, 4), (3072, 16), (8192, 64), (16384, 128)]:
         p = L.deig_default_subspace(d, k)

@@ -18,25 +18,73 @@ P_TOL = 1e-4
 EV_TOL = 1e-5
 
 
-def _syrk_check(X32, cuda, rel=2e-6):
+def _split3_tol(n):
+    # split3 per-product error <= ~3 * 2^-16 relative, zero-mean: the max
+    # elementwise error over max|S| falls like 1/sqrt(n) (CPU emulation, d = 256:
+    # 1.5e-5 at n = 1, 4e-6 at 8, 1.6e-6 at 64, 3.5e-7 at 4096; the max over
+    # more entries (larger d) sits higher).  "auto" uses split3 only for n >= 1024.
+    return 2e-6 if n >= 1024 else (5e-6 if n >= 64 else 2e-5)
+
+
+def _syrk_check(X32, cuda, rel=2e-6, algo="auto"):
     import distributed_eigenspaces_amd as de
     x = torch.from_numpy(X32).to(cuda)
-    S = de.sigma_hat(x)
+    S = de.sigma_hat(x, algo=algo)
     torch.cuda.synchronize()
     Sg = S.cpu().numpy().astype(np.float64)
     Sr = ref_cpu.sigma_hat(X32.astype(np.float64))
     err = np.abs(Sg - Sr).max() / max(np.abs(Sr).max(), 1e-300)
-    assert err <= rel, f"SYRK rel err {err:.3e} (n={X32.shape[0]}, d={X32.shape[1]})"
+    assert err <= rel, f"SYRK[{algo}] rel err {err:.3e} (n={X32.shape[0]}, d={X32.shape[1]})"
     assert np.array_equal(Sg, Sg.T), "SYRK output must be bit-exactly symmetric"
     return Sg
 
 
-@pytest.mark.parametrize("n,d", [(1, 4), (7, 12), (33, 64), (100, 256), (257, 260), (1000, 520),
-                                 (4097, 1000), (64, 5632), (40, 7424)])
-def test_syrk_shapes(n, d, cuda):
+SYRK_SHAPES = [(1, 4), (7, 12), (33, 64), (100, 256), (257, 260), (1000, 520), (4097, 1000),
+               (64, 5632), (40, 7424), (2048, 3072)]
+
+
+@pytest.mark.parametrize("algo", ["auto", "fp32", "split3"])
+@pytest.mark.parametrize("n,d", SYRK_SHAPES)
+def test_syrk_shapes(n, d, algo, cuda):
     rng = np.random.default_rng(n * 7919 + d)
     X = rng.standard_normal((n, d)).astype(np.float32)
-    _syrk_check(X, cuda)
+    tol = _split3_tol(n) if algo == "split3" or (algo == "auto" and n >= 1024) else 2e-6
+    _syrk_check(X, cuda, rel=tol, algo=algo)
+
+
+def test_syrk_split3_chunked_accumulation(cuda):
+    """A workspace that holds one 32-row chunk: the split3 path then runs
+    ceil(n/32) split + SYRK + diagonal-correction rounds accumulating into S."""
+    import ctypes
+    from distributed_eigenspaces_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(11)
+    n, d = 1000, 300
+    X = (rng.standard_normal((n, d)) * 3 + 1).astype(np.float32)
+    x = torch.from_numpy(X).to(cuda)
+    S = torch.empty((d, d), dtype=torch.float32, device=cuda)
+    nbytes = L.deig_syrk_workspace_ex(32, d, _lib.DEIG_SYRK_SPLIT3)  # one 32-row chunk
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=cuda)
+    rc = L.deig_syrk_f32_ex(x.data_ptr(), n, d, d, ctypes.c_float(1.0 / n), S.data_ptr(), d,
+                            _lib.DEIG_SYRK_SPLIT3, ws.data_ptr(), nbytes,
+                            torch.cuda.current_stream().cuda_stream)
+    _lib.check(rc, "deig_syrk_f32_ex")
+    Sg = S.cpu().numpy().astype(np.float64)
+    Sr = ref_cpu.sigma_hat(X.astype(np.float64))
+    assert np.abs(Sg - Sr).max() <= 2e-6 * np.abs(Sr).max()
+    assert np.array_equal(Sg, Sg.T)
+    # too small a workspace is an error, not a silent fallback
+    rc = L.deig_syrk_f32_ex(x.data_ptr(), n, d, d, ctypes.c_float(1.0 / n), S.data_ptr(), d,
+                            _lib.DEIG_SYRK_SPLIT3, ws.data_ptr(), 1024,
+                            torch.cuda.current_stream().cuda_stream)
+    assert rc == _lib.DEIG_EWORKSPACE
+
+
+def test_syrk_split3_integer_data_exact_split(cuda):
+    """CIFAR-like 0..255 integers are exact in bf16 (lo = 0): split3 == fp32 sums."""
+    rng = np.random.default_rng(12)
+    X = rng.integers(0, 256, size=(3000, 1024)).astype(np.float32)
+    _syrk_check(X, cuda, rel=2e-6, algo="split3")
 
 
 def test_syrk_strided_rows(cuda):
@@ -49,15 +97,16 @@ def test_syrk_strided_rows(cuda):
     assert np.abs(S - Sr).max() <= 2e-6 * np.abs(Sr).max()
 
 
+@pytest.mark.parametrize("algo", ["auto", "fp32", "split3"])
 @pytest.mark.parametrize("name", golden_names())
-def test_worker_path_golden(name, cuda):
+def test_worker_path_golden(name, algo, cuda):
     """Sigma_hat + top-k of every shard vs the reference's own outputs."""
     import distributed_eigenspaces_amd as de
     g = load_golden(name)
     X32 = g["X"].astype(np.float32)
     k = int(g["k"])
     for i, (lo, hi) in enumerate(g["ranges"]):
-        S = de.sigma_hat(torch.from_numpy(X32[lo:hi]).to(cuda))
+        S = de.sigma_hat(torch.from_numpy(X32[lo:hi]).to(cuda), algo=algo)
         r = de.topk_eigh(S, k)
         V = r.V.cpu().numpy().astype(np.float64)
         ev = r.evals.cpu().numpy().astype(np.float64)
