@@ -16,18 +16,22 @@
 //
 // Pipeline per row chunk (bounded workspace; chunks accumulate into S):
 //   split_kernel   X (fp32, HBM) -> XP: bf16 hi/lo image in MFMA operand order,
-//                  [octet of 8 rows][hi|lo][feature (padded to 256)][8 rows],
+//                  [32-row block][256-feature panel][slice = (octet, hi|lo)]
+//                  [feature][8 rows] - a panel's K-tile is 32 contiguous KiB -
 //                  rows padded with zeros to a multiple of 32, + lo^2 partials;
 //   syrks_kernel   persistent, one 512-thread block per CU, 256 x 256 lower
-//                  tiles, v_mfma_f32_32x32x16_bf16, K-tile = 32 rows whose two
-//                  panels (32 KiB each: 4 octets x {hi, lo} x 256 features x 16 B)
-//                  are DMA'd HBM -> LDS with buffer_load ... lds, double-buffered
-//                  (128 KiB); conflict-free ds_read_b128 operand reads;
+//                  tiles, v_mfma_f32_32x32x16_bf16, K-tile = 16 rows whose two
+//                  panels (16 KiB each: 2 octets x {hi, lo} x 256 features x 16 B)
+//                  are DMA'd L2/HBM -> LDS with buffer_load ... lds into a
+//                  5-stage ring (160 KiB, 3 K-tiles in flight, counted vmcnt +
+//                  raw s_barrier); conflict-free ds_read_b128 operand reads;
 //   syrks_reduce   split-K remainder tiles, summed in block order (deterministic);
 //   diag_corr      S[i][i] += alpha * sum lo_i^2.
-// Tile order: 4 x 8 super-tiles of the lower triangle, so the ~32 tiles an XCD
+// Tile order: 8 x 4 super-tiles of the lower triangle, so the ~32 tiles an XCD
 // runs concurrently share few panels in its L2.  Work decomposition (phases +
 // K-split remainder, no atomics) is the one of syrk.hip.
+#include <cstdlib>
+
 #include "deig_internal.hpp"
 
 namespace deig {
@@ -38,15 +42,13 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BT = 256;                      // tile edge (features)
-constexpr int BK = 32;                       // rows per K-tile
+constexpr int ROWS_PAD = 32;                 // chunk rows are padded to this (2 k-steps)
 constexpr int NTHR = 512;                    // 8 waves: 2 (i) x 4 (j), wave tile 128 x 64
 constexpr int SLICE_B = BT * 16;             // (octet, hi|lo) slice of a panel: 4 KiB
-constexpr int PANEL_B = (BK / 8) * 2 * SLICE_B;  // 32 KiB
-constexpr int BUF_B = 2 * PANEL_B;           // panels A | B: 64 KiB
 constexpr int SLAB = BT * BT;                // floats per partial slab
-constexpr int FLUSH_KT = 128;                // two-level fp32 summation every 4096 rows
 constexpr int SPLIT_YB = 256;                // row groups of the split pass
-constexpr int SUPER_H = 4, SUPER_W = 8;      // super-tile shape (tiles)
+constexpr int SUPER_H = 8, SUPER_W = 4;      // super-tile shape (tiles)
+constexpr int BLOCK_B = 8 * SLICE_B;         // one panel of a 32-row block: 32 KiB
 // Recommended XP image per chunk: a config-3 shard (2^21 x 8192) in one chunk on
 // a 288 GB MI355X; callers with less room pass a smaller workspace and get chunks.
 constexpr size_t DEFAULT_CHUNK_BYTES = size_t(64) << 30;
@@ -94,93 +96,211 @@ __device__ __forceinline__ void dma16(i32x4 rsrc, int voff, const void* lds_dst)
                : "memory", "m0");
 }
 
-__device__ __forceinline__ void kt_barrier() {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-}
+// A K-tile is KT MFMA k-steps (16 rows each); the LDS ring holds NST K-tiles.
+// Panel slice sl = (octet sl/2, hi|lo sl%2) is 4 KiB = four 1-KiB DMA wave-
+// instructions; a panel has 4*KT slices.  One wave issues 4*KT DMAs per stage
+// off the diagonal (the flattened [A slices | B slices] list split over the 8
+// waves) and 2*KT on it (A only) - the counted vmcnt waits rely on these counts.
+template <int KT>
+struct Geo {
+  static constexpr int NSLICE = 4 * KT;
+  static constexpr int PANEL_B = NSLICE * SLICE_B;
+  static constexpr int BUF_B = 2 * PANEL_B;
+  static constexpr int DMA = 4 * KT, DMA_DIAG = 2 * KT;
+  static constexpr int FLUSH = 4096 / (16 * KT);  // two-level fp32 summation every 4096 rows
+};
 
-// K-tile kt of panels i0 (-> A) and j0 (-> B).  Wave w moves slice w = (octet
-// w/2, hi|lo w%2) of each panel: 4 KiB = four 1-KiB wave-instructions.
+template <int KT>
 __device__ __forceinline__ void stage(const SSched& s, int64_t kt, int i0, int j0, bool diag,
-                                     unsigned char* buf, int wave, int lane16) {
-  const i32x4 rsrc = make_rsrc(s.XP + kt * (int64_t)(BK / 8) * 2 * s.dp * 16,
-                               (uint32_t)((BK / 8) * 2 * s.dp * 16));
+                                      unsigned char* buf, int wave, int lane16) {
+  using G_ = Geo<KT>;
+  // XP: [32-row block][panel][slice 0..7][256 features][16 B]; this K-tile is
+  // slices s0 .. s0 + 4*KT - 1 of block kt*KT/2.
+  const int64_t blk = kt * KT / 2;
+  const int s0 = (int)((kt * KT) & 1) * 4;
+  const i32x4 rsrc = make_rsrc(s.XP + blk * (int64_t)s.nt * BLOCK_B, (uint32_t)(s.nt * BLOCK_B));
   int l16 = lane16;
   asm volatile("" : "+v"(l16));
-  const int sl = (int)(wave * s.dp) * 16;  // slice base in the K-tile image
-  unsigned char* dA = buf + wave * SLICE_B;
-#pragma unroll
-  for (int p = 0; p < 4; ++p) dma16(rsrc, l16 + sl + i0 * 16 + p * 1024, dA + p * 1024);
   if (!diag) {
-    unsigned char* dB = buf + PANEL_B + wave * SLICE_B;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) dma16(rsrc, l16 + sl + j0 * 16 + p * 1024, dB + p * 1024);
+    for (int u = 0; u < KT; ++u) {
+      const int c = wave * KT + u;  // slice in [A slices | B slices]
+      const int pb = c / G_::NSLICE, sl = c % G_::NSLICE;
+      const int g = (pb ? j0 : i0) / BT * BLOCK_B + (s0 + sl) * SLICE_B;
+      unsigned char* dst = buf + pb * G_::PANEL_B + sl * SLICE_B;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) dma16(rsrc, l16 + g + p * 1024, dst + p * 1024);
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < 2 * KT; ++u) {
+      const int idx = wave * 2 * KT + u;  // (slice, 1-KiB part) of panel A
+      const int sl = idx >> 2, p = idx & 3;
+      dma16(rsrc, l16 + i0 / BT * BLOCK_B + (s0 + sl) * SLICE_B + p * 1024,
+            buf + sl * SLICE_B + p * 1024);
+    }
   }
 }
 
-__device__ __forceinline__ void compute(const unsigned char* A, const unsigned char* B,
-                                        f32x16 (&acc)[4][2], int wi, int wj, int lane) {
-  const int c = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int st = 0; st < BK / 16; ++st) {
-    const int o = 2 * st + h;  // octet this lane's 8 k-values come from
-    const unsigned char* ph = A + ((o * 2) * BT + 128 * wi + c) * 16;
-    const unsigned char* qh = B + ((o * 2) * BT + 64 * wj + c) * 16;
-    bf16x8 ahi[4], alo[4], bhi[2], blo[2];
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb) {
-      ahi[mb] = *reinterpret_cast<const bf16x8*>(ph + (32 * mb) * 16);
-      alo[mb] = *reinterpret_cast<const bf16x8*>(ph + (BT + 32 * mb) * 16);
-    }
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      bhi[nb] = *reinterpret_cast<const bf16x8*>(qh + (32 * nb) * 16);
-      blo[nb] = *reinterpret_cast<const bf16x8*>(qh + (BT + 32 * nb) * 16);
-    }
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Wait until this wave's DMAs of a stage have landed while `ahead` later stages
+// (0 .. NST-2) may stay in flight.
+template <int KT, int NST>
+__device__ __forceinline__ void wait_stage(int ahead, bool diag) {
+  static_assert(NST >= 2 && NST <= 5, "ring depth");
+  constexpr int D = Geo<KT>::DMA, DD = Geo<KT>::DMA_DIAG;
+  if (ahead <= 0) {
+    wait_vm<0>();
+  } else if (ahead == 1 || NST == 3) {
+    if (diag) wait_vm<DD>(); else wait_vm<D>();
+  } else if (ahead == 2 || NST == 4) {
+    if (diag) wait_vm<2 * DD>(); else wait_vm<2 * D>();
+  } else {
+    if (diag) wait_vm<3 * DD>(); else wait_vm<3 * D>();
+  }
+}
+
+// ---------------------------------------------------------------- accumulators
+// A wave's 128 x 64 output tile in MFMA result registers, for two MFMA shapes:
+//   MF = 32: v_mfma_f32_32x32x16_bf16, 4 x 2 blocks of f32x16;
+//   MF = 16: v_mfma_f32_16x16x32_bf16, 8 x 4 blocks of f32x4.
+// Both are viewed as 32 "quads": 4 consecutive rows ib..ib+3 of one column j,
+// which is how they are flushed, spilled to slabs and stored.
+template <int MF>
+struct Acc;
+
+template <>
+struct Acc<32> {
+  f32x16 a[4][2];
+  __device__ __forceinline__ void zero() {
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-      for (int nb = 0; nb < 2; ++nb) {
-        acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[mb], bhi[nb], acc[mb][nb], 0, 0, 0);
-        acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[mb], blo[nb], acc[mb][nb], 0, 0, 0);
-        acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[mb], bhi[nb], acc[mb][nb], 0, 0, 0);
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) a[mb][nb][r] = 0.f;
+  }
+  // quad q = (mb, nb, g): rows 32 mb + 8 g + 4 (lane / 32), column 32 nb + lane % 32
+  __device__ __forceinline__ float at(int q, int u) const { return a[q >> 3][(q >> 2) & 1][4 * (q & 3) + u]; }
+  __device__ __forceinline__ void set(int q, int u, float v) { a[q >> 3][(q >> 2) & 1][4 * (q & 3) + u] = v; }
+  static __device__ __forceinline__ int qrow(int q, int lane) {
+    return 32 * (q >> 3) + 8 * (q & 3) + 4 * (lane >> 5);
+  }
+  static __device__ __forceinline__ int qcol(int q, int lane) { return 32 * ((q >> 2) & 1) + (lane & 31); }
+
+  // One K-tile of KT 16-row k-steps; operand slice of 8 k-values: octet 2 st + lane / 32.
+  template <int KT>
+  __device__ __forceinline__ void mma(const unsigned char* A, const unsigned char* B, int wi,
+                                      int wj, int lane) {
+    const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int st = 0; st < KT; ++st) {
+      const int o = 2 * st + h;
+      const unsigned char* ph = A + ((o * 2) * BT + 128 * wi + c) * 16;
+      const unsigned char* qh = B + ((o * 2) * BT + 64 * wj + c) * 16;
+      bf16x8 ahi[4], alo[4], bhi[2], blo[2];
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) {
+        ahi[mb] = *reinterpret_cast<const bf16x8*>(ph + (32 * mb) * 16);
+        alo[mb] = *reinterpret_cast<const bf16x8*>(ph + (BT + 32 * mb) * 16);
       }
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        bhi[nb] = *reinterpret_cast<const bf16x8*>(qh + (32 * nb) * 16);
+        blo[nb] = *reinterpret_cast<const bf16x8*>(qh + (BT + 32 * nb) * 16);
+      }
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+          a[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[mb], bhi[nb], a[mb][nb], 0, 0, 0);
+          a[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[mb], blo[nb], a[mb][nb], 0, 0, 0);
+          a[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[mb], bhi[nb], a[mb][nb], 0, 0, 0);
+        }
+    }
+  }
+};
+
+template <>
+struct Acc<16> {
+  f32x4 a[8][4];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) a[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // quad q = (mb, nb): rows 16 mb + 4 (lane / 16), column 16 nb + lane % 16
+  __device__ __forceinline__ float at(int q, int u) const { return a[q >> 2][q & 3][u]; }
+  __device__ __forceinline__ void set(int q, int u, float v) { a[q >> 2][q & 3][u] = v; }
+  static __device__ __forceinline__ int qrow(int q, int lane) { return 16 * (q >> 2) + 4 * (lane >> 4); }
+  static __device__ __forceinline__ int qcol(int q, int lane) { return 16 * (q & 3) + (lane & 15); }
+
+  // One K-tile of KT 16-row k-steps = KT/2 32-deep MFMA steps; operand slice of
+  // 8 k-values: octet 4 st + lane / 16 (conflict-free ds_read_b128 lane groups).
+  template <int KT>
+  __device__ __forceinline__ void mma(const unsigned char* A, const unsigned char* B, int wi,
+                                      int wj, int lane) {
+    static_assert(KT % 2 == 0, "16x16x32 needs 32-row K-tiles");
+    const int c = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int st = 0; st < KT / 2; ++st) {
+      const int o = 4 * st + g;
+      const unsigned char* ph = A + ((o * 2) * BT + 128 * wi + c) * 16;
+      const unsigned char* qh = B + ((o * 2) * BT + 64 * wj + c) * 16;
+      bf16x8 bhi[4], blo[4];
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        bhi[nb] = *reinterpret_cast<const bf16x8*>(qh + (16 * nb) * 16);
+        blo[nb] = *reinterpret_cast<const bf16x8*>(qh + (BT + 16 * nb) * 16);
+      }
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) {
+        const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(ph + (16 * mb) * 16);
+        const bf16x8 alo = *reinterpret_cast<const bf16x8*>(ph + (BT + 16 * mb) * 16);
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) {
+          a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi[nb], a[mb][nb], 0, 0, 0);
+          a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, blo[nb], a[mb][nb], 0, 0, 0);
+          a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bhi[nb], a[mb][nb], 0, 0, 0);
+        }
+      }
+    }
+  }
+};
+
+constexpr int NQUAD = 32;
+
+// Slab image: quad-major, 16 B per lane (the reduce kernel reads it back).
+__device__ __forceinline__ f32x4* slab_at(float* slab, int wave, int q, int lane) {
+  return reinterpret_cast<f32x4*>(slab + ((wave * NQUAD + q) * 64 + lane) * 4);
+}
+
+template <int MF>
+__device__ __forceinline__ void flush(float* slab, bool first, Acc<MF>& acc, int wave, int lane) {
+#pragma unroll
+  for (int q = 0; q < NQUAD; ++q) {
+    f32x4* ptr = slab_at(slab, wave, q, lane);
+    f32x4 v = {acc.at(q, 0), acc.at(q, 1), acc.at(q, 2), acc.at(q, 3)};
+    if (!first) v += *ptr;
+    *ptr = v;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc.set(q, u, 0.f);
   }
 }
 
-__device__ __forceinline__ f32x4* slab_at(float* slab, int wave, int mb, int nb, int g, int lane) {
-  return reinterpret_cast<f32x4*>(slab + ((((wave * 4 + mb) * 2 + nb) * 4 + g) * 64 + lane) * 4);
-}
-
-__device__ __forceinline__ void flush(float* slab, bool first, f32x16 (&acc)[4][2], int wave,
-                                      int lane) {
+template <int MF>
+__device__ __forceinline__ void unflush(float* slab, Acc<MF>& acc, int wave, int lane) {
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
+  for (int q = 0; q < NQUAD; ++q) {
+    const f32x4 v = *slab_at(slab, wave, q, lane);
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        f32x4* ptr = slab_at(slab, wave, mb, nb, g, lane);
-        f32x4 v = {acc[mb][nb][4 * g], acc[mb][nb][4 * g + 1], acc[mb][nb][4 * g + 2],
-                   acc[mb][nb][4 * g + 3]};
-        if (!first) v += *ptr;
-        *ptr = v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[mb][nb][4 * g + e] = 0.f;
-      }
-}
-
-__device__ __forceinline__ void unflush(float* slab, f32x16 (&acc)[4][2], int wave, int lane) {
-#pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 v = *slab_at(slab, wave, mb, nb, g, lane);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[mb][nb][4 * g + e] += v[e];
-      }
+    for (int u = 0; u < 4; ++u) acc.set(q, u, acc.at(q, u) + v[u]);
+  }
 }
 
 // Store 4 consecutive rows ib..ib+3 of column j (values = alpha * a[u] (+ S)),
@@ -210,6 +330,7 @@ __device__ __forceinline__ void store4(const SSched& s, int ib, int j, bool diag
   }
 }
 
+template <int MF, int KT, int NST>
 __device__ void segment(const SSched& s, unsigned char* lds, int tile, int64_t k0, int64_t k1,
                         int slot, bool partial) {
   const int lane = threadIdx.x & 63;
@@ -221,64 +342,65 @@ __device__ void segment(const SSched& s, unsigned char* lds, int tile, int64_t k
   const int i0 = ti * BT, j0 = tj * BT;
   const bool diag = (ti == tj);
 
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[mb][nb][r] = 0.0f;
-
+  Acc<MF> acc;
+  acc.zero();
   float* slab = partial ? s.part + (int64_t)slot * SLAB : s.accs + (int64_t)blockIdx.x * SLAB;
   bool flushed = false;
-  if (k0 < k1) {
-    stage(s, k0, i0, j0, diag, lds, wave, lane16);
-    kt_barrier();
-    int cur = 0, since = 0;
-    for (int64_t kt = k0; kt < k1; ++kt) {
+  const int64_t nkt = k1 - k0;
+  if (nkt > 0) {
+    // Nothing else may be in flight on the VM counter while the ring runs (the
+    // counted waits assume only DMAs): drain the previous segment's stores.
+    wait_vm<0>();
+    __syncthreads();  // the previous segment's last stage may still be read
+    // Ring of NST stages; NST - 1 K-tiles are issued ahead of the one being
+    // computed.  Stage t lives in buffer t % NST.
+    constexpr int BUF_B = Geo<KT>::BUF_B;
+    for (int t = 0; t < NST - 1 && t < nkt; ++t)
+      stage<KT>(s, k0 + t, i0, j0, diag, lds + t * BUF_B, wave, lane16);
+    int cur = 0, nxt = NST - 1, since = 0;
+    for (int64_t t = 0; t < nkt; ++t) {
+      const int64_t left = nkt - 1 - t;
+      // RAW: this wave's DMAs of stage t landed (counted vmcnt), then a barrier
+      // every reader passes.  WAR: stage t-1's ds_reads retired (lgkmcnt) before
+      // the barrier, so its buffer can be restaged right after it.  A raw
+      // s_barrier: __syncthreads() would drain the ring with vmcnt(0).
+      wait_stage<KT, NST>(left < NST - 2 ? (int)left : NST - 2, diag);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (t + NST - 1 < nkt)
+        stage<KT>(s, k0 + t + NST - 1, i0, j0, diag, lds + nxt * BUF_B, wave, lane16);
       unsigned char* bc = lds + cur * BUF_B;
-      unsigned char* bn = lds + (cur ^ 1) * BUF_B;
-      if (kt + 1 < k1) stage(s, kt + 1, i0, j0, diag, bn, wave, lane16);
-      compute(bc, diag ? bc : bc + PANEL_B, acc, wi, wj, lane);
-      if (++since == FLUSH_KT && kt + 1 < k1) {
-        flush(slab, !flushed, acc, wave, lane);
+      acc.template mma<KT>(bc, diag ? bc : bc + Geo<KT>::PANEL_B, wi, wj, lane);
+      if (++since == Geo<KT>::FLUSH && t + 1 < nkt) {
+        flush<MF>(slab, !flushed, acc, wave, lane);
+        wait_vm<0>();  // keep the slab traffic off the ring's counted waits
         flushed = true;
         since = 0;
       }
-      kt_barrier();
-      cur ^= 1;
+      cur = cur + 1 == NST ? 0 : cur + 1;
+      nxt = nxt + 1 == NST ? 0 : nxt + 1;
     }
   }
-  if (flushed) unflush(slab, acc, wave, lane);
+  if (flushed) unflush<MF>(slab, acc, wave, lane);
 
   if (partial) {
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          f32x4 v = {acc[mb][nb][4 * g], acc[mb][nb][4 * g + 1], acc[mb][nb][4 * g + 2],
-                     acc[mb][nb][4 * g + 3]};
-          *slab_at(slab, wave, mb, nb, g, lane) = v;
-        }
+    for (int q = 0; q < NQUAD; ++q)
+      *slab_at(slab, wave, q, lane) = f32x4{acc.at(q, 0), acc.at(q, 1), acc.at(q, 2), acc.at(q, 3)};
     return;
   }
-  const int c = lane & 31, h = lane >> 5;
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float a[4] = {acc[mb][nb][4 * g], acc[mb][nb][4 * g + 1], acc[mb][nb][4 * g + 2],
-                            acc[mb][nb][4 * g + 3]};
-        store4(s, i0 + 128 * wi + 32 * mb + 8 * g + 4 * h, j0 + 64 * wj + 32 * nb + c, diag, a);
-      }
+  for (int q = 0; q < NQUAD; ++q) {
+    const float a[4] = {acc.at(q, 0), acc.at(q, 1), acc.at(q, 2), acc.at(q, 3)};
+    store4(s, i0 + 128 * wi + Acc<MF>::qrow(q, lane), j0 + 64 * wj + Acc<MF>::qcol(q, lane), diag, a);
+  }
 }
 
+template <int MF, int KT, int NST>
 __global__ __launch_bounds__(NTHR) void syrks_kernel(SSched s) {
-  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * BUF_B];
+  static_assert(NST * Geo<KT>::BUF_B <= 160 * 1024, "LDS ring exceeds 160 KiB");
+  __shared__ __attribute__((aligned(16))) unsigned char lds[NST * Geo<KT>::BUF_B];
   const int b = blockIdx.x;
   const int L = xcd_logical(b, s.G);
   int64_t pos = 0, end = 0;
@@ -310,16 +432,17 @@ __global__ __launch_bounds__(NTHR) void syrks_kernel(SSched s) {
     } else {
       break;
     }
-    segment(s, lds, tile, k0, k1, slot, partial);
+    segment<MF, KT, NST>(s, lds, tile, k0, k1, slot, partial);
   }
 }
 
 // grid (R, SLAB/4/256): one thread per float4 of a remainder tile's slab image.
+template <int MF>
 __global__ __launch_bounds__(256) void syrks_reduce_kernel(SSched s) {
   const int r = blockIdx.x;
   const int f = blockIdx.y * 256 + threadIdx.x;
-  const int lane = f & 63, g = (f >> 6) & 3, nb = (f >> 8) & 1, mb = (f >> 9) & 3, wave = f >> 11;
-  const int wi = wave >> 2, wj = wave & 3, c = lane & 31, h = lane >> 5;
+  const int lane = f & 63, q = (f >> 6) & (NQUAD - 1), wave = f >> 11;
+  const int wi = wave >> 2, wj = wave & 3;
   const int tt = s.order[s.q * s.G + r];
   const int ti = tt & 0xffff, tj = tt >> 16;
   const bool diag = (ti == tj);
@@ -333,7 +456,8 @@ __global__ __launch_bounds__(256) void syrks_reduce_kernel(SSched s) {
     sum += *reinterpret_cast<const f32x4*>(s.part + slot * SLAB + (int64_t)f * 4);
   }
   const float a[4] = {sum[0], sum[1], sum[2], sum[3]};
-  store4(s, ti * BT + 128 * wi + 32 * mb + 8 * g + 4 * h, tj * BT + 64 * wj + 32 * nb + c, diag, a);
+  store4(s, ti * BT + 128 * wi + Acc<MF>::qrow(q, lane), tj * BT + 64 * wj + Acc<MF>::qcol(q, lane),
+         diag, a);
 }
 
 __device__ __forceinline__ uint32_t bf16_rne(float x) {
@@ -378,8 +502,11 @@ __global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ X,
         lv[p] = l0 | (l1 << 16);
       }
       const int64_t f = fb + lane + 64 * q;
-      *reinterpret_cast<u32x4*>(XP + ((o * 2 + 0) * dp + f) * 16) = hv;
-      *reinterpret_cast<u32x4*>(XP + ((o * 2 + 1) * dp + f) * 16) = lv;
+      // [32-row block o/4][panel f/256][slice (o%4)*2 + hi|lo][f%256][16 B]
+      unsigned char* dst = XP + ((o >> 2) * (dp / BT) + (f / BT)) * BLOCK_B +
+                           ((o & 3) * 2) * SLICE_B + (f % BT) * 16;
+      *reinterpret_cast<u32x4*>(dst) = hv;
+      *reinterpret_cast<u32x4*>(dst + SLICE_B) = lv;
     }
   }
 #pragma unroll
@@ -446,9 +573,9 @@ Layout make_layout(int64_t n, int64_t d, int G, int64_t chunk_rows) {
 
 int64_t default_chunk_rows(int64_t n, int64_t d) {
   const int64_t dp = cdiv(d, BT) * BT;
-  const int64_t n32 = cdiv(n, BK) * BK;
-  int64_t cap = (int64_t)(DEFAULT_CHUNK_BYTES / (size_t)(dp * 4)) / BK * BK;
-  if (cap < BK) cap = BK;
+  const int64_t n32 = cdiv(n, ROWS_PAD) * ROWS_PAD;
+  int64_t cap = (int64_t)(DEFAULT_CHUNK_BYTES / (size_t)(dp * 4)) / ROWS_PAD * ROWS_PAD;
+  if (cap < ROWS_PAD) cap = ROWS_PAD;
   return n32 < cap ? n32 : cap;
 }
 
@@ -471,11 +598,11 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
   const int G = num_cus();
   // Largest chunk (multiple of 32 rows, <= n rounded up) that fits the workspace.
   Layout L0 = make_layout(n, d, G, 0);
-  if (!ws || ws_bytes < L0.total + (size_t)BK * L0.dp * 4)
+  if (!ws || ws_bytes < L0.total + (size_t)ROWS_PAD * L0.dp * 4)
     return fail(DEIG_EWORKSPACE, "syrk: workspace %zu bytes < minimum %zu", ws_bytes,
-                L0.total + (size_t)BK * L0.dp * 4);
-  int64_t chunk = (int64_t)((ws_bytes - L0.total) / (size_t)(L0.dp * 4)) / BK * BK;
-  const int64_t n32 = cdiv(n, BK) * BK;
+                L0.total + (size_t)ROWS_PAD * L0.dp * 4);
+  int64_t chunk = (int64_t)((ws_bytes - L0.total) / (size_t)(L0.dp * 4)) / ROWS_PAD * ROWS_PAD;
+  const int64_t n32 = cdiv(n, ROWS_PAD) * ROWS_PAD;
   if (chunk > n32) chunk = n32;
   const Layout L = make_layout(n, d, G, chunk);
   char* base = static_cast<char*>(ws);
@@ -498,13 +625,20 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
   float* corr = reinterpret_cast<float*>(base + L.off_corr);
   unsigned char* xp = reinterpret_cast<unsigned char*>(base + L.off_xp);
 
+  // Kernel shape: MFMA 16x16x32 (variant 162) or 32x32x16 (22: 2 k-steps per
+  // K-tile x 2 stages; 13 | 14 | 15: 1 k-step x 3 | 4 | 5 stages).
+  // DEIG_SYRK_VARIANT selects one for A/B measurements.
+  int variant = 162;
+  if (const char* v = getenv("DEIG_SYRK_VARIANT")) variant = atoi(v);
   hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(64), 0, stream, s.nt,
                      reinterpret_cast<int*>(base + L.off_order));
   DEIG_HIP_CHECK(hipGetLastError());
   for (int64_t r0 = 0, c = 0; r0 < n; r0 += chunk, ++c) {
     const int64_t rows = (n - r0) < chunk ? (n - r0) : chunk;
-    const int64_t nk = cdiv(rows, BK);
-    const int64_t noct = nk * (BK / 8);
+    const int64_t nk32 = cdiv(rows, ROWS_PAD);  // 32-row blocks (zero-padded)
+    const int64_t noct = nk32 * (ROWS_PAD / 8);
+    const int kt_steps = (variant >= 13 && variant <= 15) ? 1 : 2;  // k-steps per K-tile
+    const int64_t nk = nk32 * (ROWS_PAD / 16) / kt_steps;
     int64_t yb = cdiv(noct, 4);
     if (yb > L.yb_max) yb = L.yb_max;
     hipLaunchKernelGGL(split_kernel, dim3((unsigned)(L.dp / 256), (unsigned)yb), dim3(256), 0,
@@ -513,10 +647,20 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
     s.NK = nk;
     s.Wr = (int64_t)s.R * nk;
     s.beta = c > 0 ? 1 : 0;
-    hipLaunchKernelGGL(syrks_kernel, dim3(G), dim3(NTHR), 0, stream, s);
+    const bool mf16 = variant >= 100;
+    switch (variant) {
+      case 13: hipLaunchKernelGGL((syrks_kernel<32, 1, 3>), dim3(G), dim3(NTHR), 0, stream, s); break;
+      case 14: hipLaunchKernelGGL((syrks_kernel<32, 1, 4>), dim3(G), dim3(NTHR), 0, stream, s); break;
+      case 15: hipLaunchKernelGGL((syrks_kernel<32, 1, 5>), dim3(G), dim3(NTHR), 0, stream, s); break;
+      case 22: hipLaunchKernelGGL((syrks_kernel<32, 2, 2>), dim3(G), dim3(NTHR), 0, stream, s); break;
+      default: hipLaunchKernelGGL((syrks_kernel<16, 2, 2>), dim3(G), dim3(NTHR), 0, stream, s); break;
+    }
     DEIG_HIP_CHECK(hipGetLastError());
     if (s.R > 0) {
-      hipLaunchKernelGGL(syrks_reduce_kernel, dim3(s.R, SLAB / 4 / 256), dim3(256), 0, stream, s);
+      if (mf16)
+        hipLaunchKernelGGL(syrks_reduce_kernel<16>, dim3(s.R, SLAB / 4 / 256), dim3(256), 0, stream, s);
+      else
+        hipLaunchKernelGGL(syrks_reduce_kernel<32>, dim3(s.R, SLAB / 4 / 256), dim3(256), 0, stream, s);
       DEIG_HIP_CHECK(hipGetLastError());
     }
     hipLaunchKernelGGL(diag_corr_kernel, dim3((unsigned)cdiv(d, 256)), dim3(256), 0, stream, corr,
