@@ -128,15 +128,31 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
     return fail(DEIG_EWORKSPACE, "solver: workspace %zu bytes < required %zu", ws_bytes, total);
 
   static const bool debug = getenv("DEIG_DEBUG") && getenv("DEIG_DEBUG")[0] == '1';
+  // Rayleigh-Ritz (Gram + small solve + update + residual check) runs on every
+  // rr_every-th sweep; the sweeps between are plain power steps Q <- A Q on the
+  // Ritz vectors of the last RR (same span as subspace iteration; the
+  // generalised RR copes with the non-orthonormal basis).  The single-workgroup
+  // small solve is the latency-bound part of a sweep, so this divides its cost.
+  static const int rr_every_env = getenv("DEIG_RR_EVERY") ? atoi(getenv("DEIG_RR_EVERY")) : 0;
+  const int rr_every = rr_every_env > 0 ? rr_every_env : 2;
   int rc = rr_init_launch(w.rr.Z, d, p, Q0, k0, ldq0, 0x5eed5eedull, st);
   if (rc) return rc;
   float best = 3.4e38f;
   int since_best = 0;
+  int since_rr = 0;
   int it = 0;
   float last = 3.4e38f;
   bool converged = false;
   for (it = 0; it < max_sweeps; ++it) {
     if ((rc = apply_op(op, w, d, p, st))) return rc;
+    if (it > 0 && ++since_rr < rr_every && it + 1 < max_sweeps) {
+      // power step: Q <- Y (columns p..2p-1 of Z into columns 0..p-1)
+      DEIG_HIP_CHECK(hipMemcpy2DAsync(w.rr.Z, sizeof(float) * 2 * p, w.rr.Z + p,
+                                      sizeof(float) * 2 * p, sizeof(float) * p, d,
+                                      hipMemcpyDeviceToDevice, st));
+      continue;
+    }
+    since_rr = 0;
     if ((rc = skinny_launch(true, w.rr.Z, 2 * p, w.rr.Z, 2 * p, w.rr.C, 2 * p, 2 * p, 2 * p, d,
                             1.f, 0.f, w.slab, w.slab_bytes, st)))
       return rc;

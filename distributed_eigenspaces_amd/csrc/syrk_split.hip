@@ -65,6 +65,8 @@ struct SSched {
   int d, nt, T, G, q, R;
   float alpha;
   int beta;
+  int flush_kt;  // K-tiles between two-level flushes of the accumulators
+  int prio;      // 1: waves 4-7 run at s_setprio 1 (the arbitration losers otherwise)
 };
 
 __device__ __forceinline__ int xcd_logical(int b, int G) {
@@ -107,7 +109,6 @@ struct Geo {
   static constexpr int PANEL_B = NSLICE * SLICE_B;
   static constexpr int BUF_B = 2 * PANEL_B;
   static constexpr int DMA = 4 * KT, DMA_DIAG = 2 * KT;
-  static constexpr int FLUSH = 4096 / (16 * KT);  // two-level fp32 summation every 4096 rows
 };
 
 template <int KT>
@@ -253,6 +254,10 @@ struct Acc<16> {
       const unsigned char* ph = A + ((o * 2) * BT + 128 * wi + c) * 16;
       const unsigned char* qh = B + ((o * 2) * BT + 64 * wj + c) * 16;
       bf16x8 bhi[4], blo[4];
+      // A block mb + 1 is read while block mb's 12 MFMAs run (two A register
+      // sets), so only the first read of a k-step exposes LDS latency.
+      bf16x8 ahi = *reinterpret_cast<const bf16x8*>(ph);
+      bf16x8 alo = *reinterpret_cast<const bf16x8*>(ph + BT * 16);
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb) {
         bhi[nb] = *reinterpret_cast<const bf16x8*>(qh + (16 * nb) * 16);
@@ -260,14 +265,30 @@ struct Acc<16> {
       }
 #pragma unroll
       for (int mb = 0; mb < 8; ++mb) {
-        const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(ph + (16 * mb) * 16);
-        const bf16x8 alo = *reinterpret_cast<const bf16x8*>(ph + (BT + 16 * mb) * 16);
-#pragma unroll
-        for (int nb = 0; nb < 4; ++nb) {
-          a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi[nb], a[mb][nb], 0, 0, 0);
-          a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, blo[nb], a[mb][nb], 0, 0, 0);
-          a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bhi[nb], a[mb][nb], 0, 0, 0);
+        bf16x8 nhi = ahi, nlo = alo;
+        if (mb + 1 < 8) {
+          nhi = *reinterpret_cast<const bf16x8*>(ph + (16 * (mb + 1)) * 16);
+          nlo = *reinterpret_cast<const bf16x8*>(ph + (BT + 16 * (mb + 1)) * 16);
         }
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+          a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi[nb], a[mb][nb], 0, 0, 0);
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+          a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, blo[nb], a[mb][nb], 0, 0, 0);
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+          a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bhi[nb], a[mb][nb], 0, 0, 0);
+        ahi = nhi;
+        alo = nlo;
+      }
+      // Issue order for the scheduler: A0 + B reads, then per block the next
+      // block's two A reads ahead of the current block's 12 MFMAs.
+      __builtin_amdgcn_sched_group_barrier(0x100, 10, 0);
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) {
+        if (mb + 1 < 8) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
       }
     }
   }
@@ -342,6 +363,7 @@ __device__ void segment(const SSched& s, unsigned char* lds, int tile, int64_t k
   const int i0 = ti * BT, j0 = tj * BT;
   const bool diag = (ti == tj);
 
+  if (s.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
   Acc<MF> acc;
   acc.zero();
   float* slab = partial ? s.part + (int64_t)slot * SLAB : s.accs + (int64_t)blockIdx.x * SLAB;
@@ -372,7 +394,7 @@ __device__ void segment(const SSched& s, unsigned char* lds, int tile, int64_t k
         stage<KT>(s, k0 + t + NST - 1, i0, j0, diag, lds + nxt * BUF_B, wave, lane16);
       unsigned char* bc = lds + cur * BUF_B;
       acc.template mma<KT>(bc, diag ? bc : bc + Geo<KT>::PANEL_B, wi, wj, lane);
-      if (++since == Geo<KT>::FLUSH && t + 1 < nkt) {
+      if (++since == s.flush_kt && t + 1 < nkt) {
         flush<MF>(slab, !flushed, acc, wave, lane);
         wait_vm<0>();  // keep the slab traffic off the ring's counted waits
         flushed = true;
@@ -630,6 +652,14 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
   // DEIG_SYRK_VARIANT selects one for A/B measurements.
   int variant = 162;
   if (const char* v = getenv("DEIG_SYRK_VARIANT")) variant = atoi(v);
+  // Two-level fp32 summation: accumulators are added into a per-block slab
+  // every flush_rows rows (DEIG_SYRK_FLUSH_ROWS overrides, for A/B runs).
+  int64_t flush_rows = 4096;
+  if (const char* v = getenv("DEIG_SYRK_FLUSH_ROWS")) flush_rows = atoll(v);
+  if (flush_rows < 32) flush_rows = 32;
+  if (flush_rows > (int64_t(1) << 30)) flush_rows = int64_t(1) << 30;
+  s.prio = 0;
+  if (const char* v = getenv("DEIG_SYRK_PRIO")) s.prio = atoi(v);
   hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(64), 0, stream, s.nt,
                      reinterpret_cast<int*>(base + L.off_order));
   DEIG_HIP_CHECK(hipGetLastError());
@@ -647,6 +677,7 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
     s.NK = nk;
     s.Wr = (int64_t)s.R * nk;
     s.beta = c > 0 ? 1 : 0;
+    s.flush_kt = (int)(flush_rows / (16 * kt_steps));
     const bool mf16 = variant >= 100;
     switch (variant) {
       case 13: hipLaunchKernelGGL((syrks_kernel<32, 1, 3>), dim3(G), dim3(NTHR), 0, stream, s); break;

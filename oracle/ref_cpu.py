@@ -24,7 +24,7 @@ import scipy.linalg
 __all__ = [
     "sigma_hat", "top_k_eigh", "top_k_eigenvectors", "split_batches",
     "dispatch_order", "projector_average", "server_topk", "make_batches",
-    "online_notebook", "online_figure", "one_shot", "oja_epoch",
+    "online_notebook", "online_figure", "one_shot", "oja_epoch", "oja_stream",
     "projector_distance", "sin_theta", "align_signs",
 ]
 
@@ -170,6 +170,28 @@ def oja_epoch(X, V0, eta: float, batch: int):
         V = V + eta * (xb.T @ (xb @ V)) / xb.shape[0]
         V, _ = np.linalg.qr(V)
     return V
+
+
+def oja_stream(rank_batches, V0, eta: float, agg_every: int):
+    """Streaming Oja on R ranks with periodic aggregation (parity unpinned: not in
+    the reference; restates distributed_eigenspaces_amd.streaming.StreamingOja).
+
+    ``rank_batches[r]`` is rank r's list of row batches (all lists equally long).
+    Every rank starts from V0; after every ``agg_every`` batches all ranks adopt the
+    server solve of their bases (``server_topk``: top-k of (1/R) sum V_r V_r^T,
+    distributed.py:126-130 + NB:306).  Returns the rank-0 basis at the end."""
+    R = len(rank_batches)
+    k = np.asarray(V0).shape[1]
+    Vs = [np.array(V0, dtype=np.float64) for _ in range(R)]
+    for i in range(len(rank_batches[0])):
+        for r in range(R):
+            xb = np.asarray(rank_batches[r][i], dtype=np.float64)
+            v = Vs[r] + eta * (xb.T @ (xb @ Vs[r])) / xb.shape[0]
+            Vs[r], _ = np.linalg.qr(v)
+        if agg_every > 0 and (i + 1) % agg_every == 0:
+            _, vbar = server_topk(Vs, k, R)
+            Vs = [vbar.copy() for _ in range(R)]
+    return Vs[0]
 
 
 def projector_distance(A, B) -> float:
