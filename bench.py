@@ -1,28 +1,39 @@
 #!/usr/bin/env python
-"""Benchmark: one-shot distributed eigenspace estimation on MI355X.
+"""Benchmark: distributed eigenspace estimation on MI355X.
 
-Workload (BASELINE.json configs[2], the metric's "d=8192, k=64" config): each GPU
-holds one worker's shard of 2^21 synthetic spiked-covariance rows x d = 8192
-(fp32, 64 GiB, resident in HBM before timing); k = 64.  At N GPUs the job covers
-N * 2^21 rows (N = 8 -> 16,777,216 = config 3), so scaling is "weak".
+Default workload (BASELINE.json configs[2], the metric's "d=8192, k=64" config):
+each GPU holds one worker's shard of 2^21 synthetic spiked-covariance rows x
+d = 8192 (fp32, 64 GiB, resident in HBM before timing); k = 64.  At N GPUs the
+job covers N * 2^21 rows (N = 8 -> 16,777,216 = config 3), so scaling is "weak".
 
-One step = time-to-eigenspace of the whole pipeline:
-  worker: Sigma_hat = X^T X / n (SYRK kernel) -> top-k eigenpairs (subspace
-  iteration) ; exchange: all-gather of the d x k bases (RCCL, N > 1) ;
-  server: top-k of the projector average (implicit operator) on rank 0.
-value = samples ingested per second over the whole job = N * n / t_step.
+One step of a one-shot config = time-to-eigenspace of the whole pipeline:
+  workers: Sigma_hat = X^T X / n (SYRK kernel) -> top-k eigenpairs (subspace
+  iteration), W logical workers per GPU back to back ; exchange: all-gather of
+  the d x k bases (RCCL, N > 1) ; server: top-k of the projector average
+  (implicit operator) on rank 0.
+value = samples ingested per second over the whole job = N * rows / t_step.
 
-Extra objects on the JSON line: ``roofline`` (the covariance op vs the MFMA peak
-of the instructions it runs, timed with HIP events on the launch stream),
-``cpu_baseline`` (the float64 oracle on a bounded sample of the same workload,
-rank 0 at N = 1 only), ``breakdown`` and ``accuracy`` (sin theta of the server
-basis vs the planted subspace; Sigma_hat vs float64 on a sampled 16 x 16 block).
+Other configs (--config; each prints its own JSON line, the driver's default
+line is c3):
+  c2  configs[1]: d = 3072, n = 2^20 rows per GPU, k = 16, one worker per GPU;
+  c5  configs[4] (stress) per GPU: 8 logical workers x 65,536 rows, d = 16384,
+      k = 128 (64 workers on 8 GPUs); server over all workers' bases;
+  c4  configs[3] (online): per GPU a stream of 4096 x 3072 batches, Oja steps
+      (k = 32), aggregation (all-gather + server solve + broadcast) every 64
+      batches; one step = 64 batches + one aggregation.
+
+Extra objects on the JSON line: ``roofline`` (the dominant kernel vs the peak of
+the instructions it runs, timed with HIP events on the launch stream),
+``sweep`` (one subspace-iteration sweep S*Q vs the HBM roof, both sweep
+kernels), ``cpu_baseline`` (the float64 oracle on a bounded sample of the same
+workload, rank 0 at N = 1 only), ``breakdown`` and ``accuracy``.
 
 Covariance algorithm (--syrk-algo, default auto = split3 at these sizes): fp32
 samples split into bf16 hi/lo pairs, 3 bf16 MFMA products per fp32 product,
-fp32 accumulation (include/deig.h); "fp32" = the f32 MFMA kernel.
+fp32 accumulation (include/deig.h); "fp32" = the f32 MFMA kernel.  The fp32
+kernel is also timed once outside the timed region (``roofline.fp32_kernel``).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5]
        [--syrk-algo auto|split3|fp32]
        (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N)
 """
@@ -47,56 +58,116 @@ BF16_MFMA_PEAK = 2.5e15    # MI355X_MICROARCH.md: BF16 MFMA, dense (16 x the f32
 HBM_PEAK = 8.0e12
 
 CONFIGS = {
-    # name: (rows per GPU, d, k, workload label)
-    "c3": (1 << 21, 8192, 64, "synthetic spiked d=8192 k=64, 2^21 rows/GPU (config 3 shard)"),
-    "c2": (1 << 20, 3072, 16, "synthetic spiked d=3072 n=1M k=16 (config 2)"),
+    "c3": dict(kind="oneshot", rows=1 << 21, d=8192, k=64, workers=1,
+               label="synthetic spiked d=8192 k=64, 2^21 rows/GPU (config 3 shard)"),
+    "c2": dict(kind="oneshot", rows=1 << 20, d=3072, k=16, workers=1,
+               label="synthetic spiked d=3072 n=2^20 k=16 per GPU (config 2)"),
+    "c5": dict(kind="oneshot", rows=8 * 65536, d=16384, k=128, workers=8,
+               label="stress: synthetic spiked d=16384 k=128, 8 logical workers x 65536 rows "
+                     "per GPU (config 5)"),
+    "c4": dict(kind="oja", rows=4096, d=3072, k=32, agg_every=64, eta=0.02, orth_every=8,
+               label="online: Oja mini-batches 4096 x 3072, k=32, aggregation every 64 "
+                     "batches (config 4)"),
 }
+EIGH_MAX_D = 8192  # CPU baseline: larger d times eigh on a leading block and scales by d^3
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(X_dev: torch.Tensor, n_full: int, k: int, sample_rows: int):
-    """Float64 oracle (oracle/ref_cpu.py) on the first ``sample_rows`` rows; the
-    covariance term is scaled linearly to the full shard (it is linear in n)."""
-    from oracle import ref_cpu
+def blas_cores():
     try:
         from threadpoolctl import threadpool_info
-        cores = max((i.get("num_threads", 1) for i in threadpool_info()
-                     if i.get("user_api") == "blas"), default=os.cpu_count())
+        return max((i.get("num_threads", 1) for i in threadpool_info()
+                    if i.get("user_api") == "blas"), default=os.cpu_count())
     except Exception:  # pragma: no cover
-        cores = os.cpu_count()
+        return os.cpu_count()
+
+
+def cpu_baseline_oneshot(X_dev: torch.Tensor, n_worker: int, workers: int, k: int,
+                         sample_rows: int):
+    """Float64 oracle (oracle/ref_cpu.py) on the first ``sample_rows`` rows of a
+    worker shard; the covariance term is scaled linearly to the full shard (it is
+    linear in n), the top-k eigh is timed once and counted per worker."""
+    from oracle import ref_cpu
     xs = X_dev[:sample_rows].double().cpu().numpy()
+    d = xs.shape[1]
     t0 = time.perf_counter()
     S = ref_cpu.sigma_hat(xs)
     t_cov = time.perf_counter() - t0
+    de = min(d, EIGH_MAX_D)
     t0 = time.perf_counter()
-    ref_cpu.top_k_eigh(S, k)
-    t_eig = time.perf_counter() - t0
-    t_full = t_cov * (n_full / sample_rows) + t_eig
+    ref_cpu.top_k_eigh(S[:de, :de], k)
+    t_eig = (time.perf_counter() - t0) * (d / de) ** 3
+    t_worker = t_cov * (n_worker / sample_rows) + t_eig
+    t_full = workers * t_worker
+    eig_note = (f"eigh top-{k} {t_eig:.2f}s" if de == d else
+                f"eigh top-{k} of the leading {de}x{de} block scaled by (d/{de})^3 -> {t_eig:.1f}s")
     return {
-        "value": n_full / t_full, "unit": "samples/s", "cores": int(cores), "kind": "port",
-        "sample": (f"float64 NumPy/SciPy oracle on {sample_rows} rows x d={xs.shape[1]} of the "
-                   f"same shard: sigma_hat {t_cov:.2f}s + eigh top-{k} {t_eig:.2f}s; covariance "
-                   f"scaled linearly to {n_full} rows -> {t_full:.1f}s per worker shard"),
+        "value": workers * n_worker / t_full, "unit": "samples/s", "cores": int(blas_cores()),
+        "kind": "port",
+        "sample": (f"float64 NumPy/SciPy oracle on {sample_rows} rows x d={d} of a worker shard: "
+                   f"sigma_hat {t_cov:.2f}s + {eig_note}; covariance scaled linearly to "
+                   f"{n_worker} rows -> {t_worker:.1f}s per worker shard, x {workers} worker(s); "
+                   f"server solve not counted"),
     }
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--rows", type=int, default=0, help="override rows per GPU")
-    ap.add_argument("--cpu-sample", type=int, default=4096)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--syrk-algo", default="auto", choices=["auto", "split3", "fp32"])
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="gloo = rehearsal of the N>1 control flow with ranks sharing one GPU")
-    args = ap.parse_args()
+def cpu_baseline_oja(pool, V0: torch.Tensor, eta: float, nb: int):
+    from oracle import ref_cpu
+    xs = np.concatenate([pool[i].double().cpu().numpy() for i in range(nb)])
+    b = pool[0].shape[0]
+    t0 = time.perf_counter()
+    ref_cpu.oja_epoch(xs, V0.double().cpu().numpy(), eta, b)
+    t = time.perf_counter() - t0
+    return {
+        "value": nb * b / t, "unit": "samples/s", "cores": int(blas_cores()), "kind": "port",
+        "sample": (f"float64 NumPy oracle oja_epoch on {nb} batches of {b} x {xs.shape[1]} "
+                   f"(k={V0.shape[1]}): {t:.2f}s; aggregation not counted"),
+    }
 
+
+def sin_theta(U: torch.Tensor, V: torch.Tensor) -> float:
+    s = torch.linalg.svdvals(U.double().t() @ V.double()).min().clamp(max=1)
+    return float(s.pow(2).neg().add(1).clamp(min=0).sqrt())
+
+
+def time_events(fn, reps: int, stream) -> float:
+    """Mean ms of fn() over reps launches, HIP events on ``stream``."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def sweep_roofline(de, S: torch.Tensor, p: int, stream) -> dict:
+    """One subspace-iteration sweep Y = S Q at the solver's p, both kernels:
+    4 d^2 bytes of S (read once), 2 d^2 p flop."""
+    d = S.shape[0]
+    g = torch.Generator(device=S.device).manual_seed(11)
+    Q = torch.randn((d, p), generator=g, device=S.device, dtype=torch.float32)
+    Y = torch.empty((d, p), device=S.device, dtype=torch.float32)
+    byt, fl = 4.0 * d * d, 2.0 * d * d * p
+    out = {"d": d, "p": p, "bound": "hbm", "algorithmic": "4 d^2 bytes (S read once), 2 d^2 p flop",
+           "peak_GBs": HBM_PEAK / 1e9}
+    for algo in ("split3", "fp32"):
+        ms = time_events(lambda: de.sym_apply(S, Q, algo=algo, out=Y), 20, stream)
+        t = ms * 1e-3
+        t_min = max(byt / HBM_PEAK, fl / (BF16_MFMA_PEAK / 3 if algo == "split3" else FP32_MFMA_PEAK))
+        out[algo] = {"us": ms * 1e3, "hbm_GBs": byt / t / 1e9, "hbm_frac": byt / t / HBM_PEAK,
+                     "fp32_equiv_tflops": fl / t / 1e12, "attainable_frac": t_min / t}
+    out["kernel"] = ("split3: split_q_kernel + sweep_kernel (+ sweep_reduce_kernel), bf16 MFMA "
+                     "16x16x32 on split S rows and Q; fp32: skinny_kernel<T> f32 MFMA 16x16x4")
+    out["solver_uses"] = "split3"
+    return out
+
+
+def init_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -111,55 +182,19 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+    return world, rank, dev
 
-    import distributed_eigenspaces_amd as de
-    from distributed_eigenspaces_amd import synthetic
-    from distributed_eigenspaces_amd.estimator import gather_bases
 
-    n, d, k, label = CONFIGS[args.config]
-    if args.rows:
-        n = args.rows
-    U = synthetic.planted_basis(d, k, seed=0, device=dev)
-    X = synthetic.spiked_samples(n, U, seed=1 + rank)
-    S = torch.empty((d, d), dtype=torch.float32, device=dev)
-    torch.cuda.synchronize()
-    m = world  # one logical worker per GPU
-    stream = torch.cuda.current_stream(dev)
-    times = {"syrk": [], "worker_eig": [], "gather": [], "server": []}
-    syrk_ev = []
-
-    def step(record: bool):
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        t0 = time.perf_counter()
-        e[0].record(stream)
-        de.sigma_hat(X, out=S, algo=args.syrk_algo)
-        e[1].record(stream)
-        r = de.topk_eigh(S, k, check_finite=False)  # synchronises the stream
-        t1 = time.perf_counter()
-        Wt_local = r.V.t().contiguous()           # k x d
-        Wt = gather_bases(Wt_local)
-        torch.cuda.synchronize(dev)
-        t2 = time.perf_counter()
-        res = None
-        if rank == 0:
-            res = de.projavg_topk(Wt, k, 1.0 / m, q0=Wt[:k].t())
-        torch.cuda.synchronize(dev)
-        t3 = time.perf_counter()
-        if record:
-            syrk_ev.append(e)
-            times["worker_eig"].append(t1 - t0)
-            times["gather"].append(t2 - t1)
-            times["server"].append(t3 - t2)
-        return r, res
-
+def timed_loop(step, args, world, dev):
     for _ in range(args.warmup):
         step(False)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    out = None
     for _ in range(args.steps):
-        r, res = step(True)
+        out = step(True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -169,81 +204,243 @@ def main():
                          device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    return elapsed, out
 
-    syrk_ms = float(np.mean([a.elapsed_time(b) for a, b in syrk_ev]))
-    flops = float(n) * d * (d + 1)  # algorithmic: lower triangle incl. diagonal
+
+def base_line(args, world, elapsed, total, dtype, config):
+    return {
+        "metric": METRIC,
+        "value": total / elapsed,
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": dtype,
+        "data": "synthetic spiked covariance (planted U, theta 8->4), generated on device",
+        "config": config,
+    }
+
+
+# ---------------------------------------------------------------- one-shot configs
+def run_oneshot(args, cfg, world, rank, dev):
+    import distributed_eigenspaces_amd as de
+    from distributed_eigenspaces_amd import synthetic
+    from distributed_eigenspaces_amd.estimator import gather_bases
+
+    n, d, k, W = cfg["rows"], cfg["d"], cfg["k"], cfg["workers"]
+    if args.rows:
+        n = args.rows
+    ni = n // W  # rows per logical worker (distributed.py:99-104 split of the rank block)
+    U = synthetic.planted_basis(d, k, seed=0, device=dev)
+    X = synthetic.spiked_samples(n, U, seed=1 + rank)
+    S = torch.empty((d, d), dtype=torch.float32, device=dev)
+    Wt_local = torch.empty((W * k, d), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    m = world * W
+    stream = torch.cuda.current_stream(dev)
+    rec = {"worker": [], "gather": [], "server": []}
+    syrk_ev = []
+
+    def step(record: bool):
+        t0 = time.perf_counter()
+        evs = []
+        r = None
+        for w in range(W):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            e[0].record(stream)
+            de.sigma_hat(X[w * ni:(w + 1) * ni], out=S, algo=args.syrk_algo)
+            e[1].record(stream)
+            r = de.topk_eigh(S, k, check_finite=False)  # synchronises the stream
+            Wt_local[w * k:(w + 1) * k].copy_(r.V.t())
+            evs.append((e, r.sweeps))
+        t1 = time.perf_counter()
+        Wt = gather_bases(Wt_local)
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        res = None
+        if rank == 0:
+            res = de.projavg_topk(Wt, k, 1.0 / m, q0=Wt[:k].t())
+        torch.cuda.synchronize(dev)
+        t3 = time.perf_counter()
+        if record:
+            syrk_ev.extend(evs)
+            rec["worker"].append(t1 - t0)
+            rec["gather"].append(t2 - t1)
+            rec["server"].append(t3 - t2)
+        return r, res
+
+    elapsed, (r, res) = timed_loop(step, args, world, dev)
+
+    syrk_ms = float(np.mean([a.elapsed_time(b) for (a, b), _ in syrk_ev]))
+    sweeps = [s for _, s in syrk_ev]
+    flops = float(ni) * d * (d + 1)  # algorithmic, per worker launch: lower triangle incl. diag
     algo = args.syrk_algo
     if algo == "auto":
-        algo = "split3" if n >= 1024 else "fp32"
+        algo = "split3" if ni >= 1024 else "fp32"
     if algo == "split3":
-        # 3 bf16 MFMA products per fp32 product; peak = dense bf16 MFMA
         mfma_flops, peak = 3.0 * flops, BF16_MFMA_PEAK
-        kernel = "covariance split3 (split_kernel + syrks_kernel + syrks_reduce_kernel + diag_corr_kernel)"
-        algorithmic = f"3 * n*d*(d+1) = {3 * flops:.4e} bf16 MFMA flop per launch (3 split products per fp32 product)"
+        kernel = ("covariance split3 (split_kernel + syrks_kernel + syrks_reduce_kernel + "
+                  "diag_corr_kernel)")
+        algorithmic = (f"3 * n*d*(d+1) = {3 * flops:.4e} bf16 MFMA flop per launch (n = {ni} rows; "
+                       f"3 split products per fp32 product)")
     else:
         mfma_flops, peak = flops, FP32_MFMA_PEAK
         kernel = "syrk_kernel (+ syrk_reduce_kernel)"
-        algorithmic = f"n*d*(d+1) = {flops:.4e} f32 MFMA flop per launch"
+        algorithmic = f"n*d*(d+1) = {flops:.4e} f32 MFMA flop per launch (n = {ni} rows)"
     achieved = mfma_flops / (syrk_ms * 1e-3)
-    # Sigma_hat vs float64 on a sampled 16 x 16 block (all n rows)
+
+    # --- outside the timed region: accuracy, alternative kernel, sweep roofline
+    Xw = X[(W - 1) * ni:W * ni]
     cols = torch.randperm(d, generator=torch.Generator().manual_seed(7))[:16].to(dev)
-    Xs = X.index_select(1, cols).double()
-    S64 = (Xs.t() @ Xs) / n
+    Xs = Xw.index_select(1, cols).double()
+    S64 = (Xs.t() @ Xs) / ni
     Sblk = S.index_select(0, cols).index_select(1, cols).double()
     sigma_err = float((Sblk - S64).abs().max() / S64.abs().max())
     del Xs
+    fp32_kernel = None
+    if algo == "split3" and not args.no_alt:
+        S2 = torch.empty_like(S)
+        ms = time_events(lambda: de.sigma_hat(Xw, out=S2, algo="fp32"), 1, stream)
+        fp32_kernel = {"kernel": "syrk_kernel (+ syrk_reduce_kernel), v_mfma_f32_32x32x2_f32",
+                       "launch_ms": ms, "tflops": flops / (ms * 1e-3) / 1e12,
+                       "frac": flops / (ms * 1e-3) / FP32_MFMA_PEAK,
+                       "max_abs_diff_vs_split3_rel": float((S2 - S).abs().max() / S.abs().max())}
+        del S2
+    p = de.default_subspace(d, k)
+    sweep = sweep_roofline(de, S, p, stream)
 
+    if rank != 0:
+        return None
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", f"pmc_syrk_{args.config}_{algo}.json")
+    if os.path.exists(pmc) and not args.rows:
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_oneshot(X, ni, W, k, min(args.cpu_sample, ni))
+    line = base_line(args, world, elapsed, float(n) * world * args.steps, "f32", {
+        "workload": cfg["label"], "rows_per_gpu": n, "total_rows": n * world, "d": d, "k": k,
+        "workers_per_gpu": W, "rows_per_worker": ni, "workers_total": m, "subspace_p": p,
+        "parallelism": f"dp{world} ({W} logical worker(s) per GPU, RCCL all-gather of bases)"})
+    line["dtype_note"] = ("fp32 in / fp32 out / fp32 accumulation; split3 covariance and sweeps "
+                          "form each fp32 product from 3 bf16 MFMA products of the split operands "
+                          "(hi*hi + hi*lo + lo*hi; covariance restores lo^2 on the diagonal); "
+                          "accuracy in accuracy.sigma_hat_rel_err_vs_f64_sampled and the solver "
+                          "residuals")
+    line["roofline"] = {"bound": "mfma", "kernel": kernel, "achieved": achieved / 1e12,
+                        "peak": peak / 1e12, "unit": "TFLOP/s", "frac": achieved / peak,
+                        "traffic": traffic, "algorithmic": algorithmic, "launch_ms": syrk_ms,
+                        "fp32_equiv_tflops": flops / (syrk_ms * 1e-3) / 1e12,
+                        "fp32_mfma_peak": FP32_MFMA_PEAK / 1e12, "fp32_kernel": fp32_kernel}
+    line["sweep"] = sweep
+    line["syrk_algo"] = algo
+    line["cpu_baseline"] = cpu
+    wk = 1e3 * float(np.mean(rec["worker"]))
+    line["breakdown"] = {"syrk_ms_per_worker": syrk_ms,
+                         "worker_eig_ms_per_worker": wk / W - syrk_ms,
+                         "worker_sweeps": sweeps[-W:],
+                         "gather_ms": 1e3 * float(np.mean(rec["gather"])),
+                         "server_ms": 1e3 * float(np.mean(rec["server"])),
+                         "server_sweeps": res.sweeps}
+    line["accuracy"] = {"sin_theta_server_vs_planted": sin_theta(U, res.V),
+                        "sin_theta_last_worker_vs_planted": sin_theta(U, r.V),
+                        "worker_resid": r.resid, "server_resid": res.resid,
+                        "sigma_hat_rel_err_vs_f64_sampled": sigma_err}
+    return line
+
+
+# ---------------------------------------------------------------- online (Oja) config
+def run_oja(args, cfg, world, rank, dev):
+    from distributed_eigenspaces_amd import synthetic
+    from distributed_eigenspaces_amd.streaming import StreamingOja
+
+    b, d, k, agg = cfg["rows"], cfg["d"], cfg["k"], cfg["agg_every"]
+    eta = args.eta if args.eta > 0 else cfg["eta"]
+    if args.rows:
+        b = args.rows
+    U = synthetic.planted_basis(d, k, seed=0, device=dev)
+    pool = synthetic.spiked_samples(agg * b, U, seed=1 + rank)  # 64 distinct batches, resident
+    g = torch.Generator(device="cpu").manual_seed(5)
+    V0 = torch.linalg.qr(torch.randn(d, k, generator=g, dtype=torch.float64))[0].float().to(dev)
+    est = StreamingOja(V0, eta=eta, agg_every=agg)
+    stream = torch.cuda.current_stream(dev)
+    ev = []
+    agg_t = []
+
+    def step(record: bool):
+        # one C call for the 64 batches, then the aggregation (gather + solve + broadcast)
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        e[0].record(stream)
+        est.block_fn(pool, est.V, est.eta, b, cfg["orth_every"])
+        e[1].record(stream)
+        est.batches_seen += agg
+        t0 = time.perf_counter()
+        est.aggregate()
+        torch.cuda.synchronize(dev)
+        if record:
+            ev.append(e)
+            agg_t.append(time.perf_counter() - t0)
+        return None
+
+    elapsed, _ = timed_loop(step, args, world, dev)
+    oja_ms = float(np.mean([a.elapsed_time(c) for a, c in ev])) / agg  # per batch
+    byt = 8.0 * b * d  # Xb read twice (Xb V, then Xb^T T)
+    achieved = byt / (oja_ms * 1e-3)
+    if rank != 0:
+        return None
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_oja([pool[i * b:(i + 1) * b] for i in range(16)], V0, eta, 16)
+    line = base_line(args, world, elapsed, float(agg * b) * world * args.steps, "f32", {
+        "workload": cfg["label"], "batch_rows": b, "d": d, "k": k, "agg_every": agg, "eta": eta,
+        "orth_every": cfg["orth_every"], "batches_per_gpu_per_step": agg,
+        "rows_per_gpu_per_step": agg * b,
+        "parallelism": f"dp{world} (one Oja stream per GPU; RCCL all-gather + broadcast of "
+                       f"bases every {agg} batches)"})
+    line["roofline"] = {"bound": "hbm", "kernel": "Oja steps (skinny NN Xb*V + skinny TN Xb^T*T "
+                        "+ CholQR2 every 8 batches), whole op per batch",
+                        "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK, "traffic": None,
+                        "algorithmic": f"8*b*d = {byt:.4e} bytes per batch (Xb read twice)",
+                        "launch_ms": oja_ms}
+    line["cpu_baseline"] = cpu
+    line["breakdown"] = {"oja_ms_per_batch": oja_ms,
+                         "aggregate_ms": 1e3 * float(np.mean(agg_t))}
+    line["accuracy"] = {"sin_theta_vs_planted": sin_theta(U, est.V),
+                        "batches_seen_per_gpu": est.batches_seen}
+    return line
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--rows", type=int, default=0, help="override rows per GPU (batch rows for c4)")
+    ap.add_argument("--eta", type=float, default=0.0, help="c4 step size (default: config's)")
+    ap.add_argument("--cpu-sample", type=int, default=4096)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-alt", action="store_true", help="skip the fp32-kernel comparison launch")
+    ap.add_argument("--syrk-algo", default="auto", choices=["auto", "split3", "fp32"])
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo = rehearsal of the N>1 control flow with ranks sharing one GPU")
+    args = ap.parse_args()
+
+    world, rank, dev = init_dist(args)
+    cfg = CONFIGS[args.config]
+    if cfg["kind"] == "oja":
+        line = run_oja(args, cfg, world, rank, dev)
+    else:
+        line = run_oneshot(args, cfg, world, rank, dev)
     if rank == 0:
-        sin_server = float(torch.linalg.svdvals(U.double().t() @ res.V.double()).min().clamp(max=1)
-                           .pow(2).neg().add(1).clamp(min=0).sqrt())
-        sin_worker = float(torch.linalg.svdvals(U.double().t() @ r.V.double()).min().clamp(max=1)
-                           .pow(2).neg().add(1).clamp(min=0).sqrt())
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", f"pmc_syrk_{args.config}_{algo}.json")
-        if os.path.exists(pmc) and not args.rows:
-            try:
-                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(X, n, k, min(args.cpu_sample, n))
-        total = float(n) * world * args.steps
-        line = {
-            "metric": METRIC,
-            "value": total / elapsed,
-            "unit": "samples/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic spiked covariance (planted U, theta 8->4), generated on device",
-            "config": {"workload": label, "rows_per_gpu": n, "total_rows": n * world, "d": d,
-                       "k": k, "workers": m, "subspace_p": de.default_subspace(d, k),
-                       "parallelism": f"dp{world} (one worker per GPU, RCCL all-gather)"},
-            "roofline": {"bound": "mfma", "kernel": kernel, "achieved": achieved / 1e12,
-                         "peak": peak / 1e12, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": traffic,
-                         "algorithmic": algorithmic, "launch_ms": syrk_ms,
-                         "fp32_equiv_tflops": flops / (syrk_ms * 1e-3) / 1e12,
-                         "fp32_mfma_peak": FP32_MFMA_PEAK / 1e12},
-            "syrk_algo": algo,
-            "cpu_baseline": cpu,
-            "breakdown": {"syrk_ms": syrk_ms,
-                          "worker_eig_ms": 1e3 * float(np.mean(times["worker_eig"])) - syrk_ms,
-                          "worker_sweeps": r.sweeps,
-                          "gather_ms": 1e3 * float(np.mean(times["gather"])),
-                          "server_ms": 1e3 * float(np.mean(times["server"])),
-                          "server_sweeps": res.sweeps},
-            "accuracy": {"sin_theta_server_vs_planted": sin_server,
-                         "sin_theta_worker0_vs_planted": sin_worker,
-                         "worker_resid": r.resid, "server_resid": res.resid,
-                         "sigma_hat_rel_err_vs_f64_sampled": sigma_err},
-        }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -1,16 +1,18 @@
 """MI355X-native distributed eigenspace estimation (drop-in for TimeEscaper/distributed_eigenspaces).
 
 Hot path (HIP, gfx950, behind the C ABI in include/deig.h):
-  * sigma_hat      - covariance SYRK on fp32 MFMA       (distributed.py:59-70)
-  * topk_eigh      - block subspace iteration + RR       (distributed.py:22-29)
-  * projavg_topk   - implicit projector-average solve    (distributed.py:126-130, NB:306)
-  * oja_step       - mini-batch Oja (online variant, config 4)
+  * sigma_hat      - covariance SYRK, split-bf16 or f32 MFMA  (distributed.py:59-70)
+  * topk_eigh      - block subspace iteration + RR            (distributed.py:22-29)
+  * sym_apply      - one solver sweep S Q (split-bf16 MFMA)
+  * projavg_topk   - implicit projector-average solve         (distributed.py:126-130, NB:306)
+  * oja_step(s)    - mini-batch Oja (online variant, config 4); streaming.StreamingOja
+                     adds the periodic all-gather / server solve / broadcast
 
 Drop-in modules: ``distributed`` (Node / SlaveNode / MasterNode / run_* / main),
 ``my_threading`` (Slave) and ``notebook`` (make_batches, top_k_eigenvectors,
 compute_segma_hat, online loop).
 """
-from .linalg import (EigResult, default_subspace, oja_step, projavg_topk, sigma_hat,  # noqa: F401
-                     stack_bases, topk_eigh)
+from .linalg import (EigResult, default_subspace, oja_step, oja_steps, projavg_topk,  # noqa: F401
+                     sigma_hat, stack_bases, sym_apply, topk_eigh)
 
 __version__ = "0.1.0"

@@ -13,7 +13,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdeig.so")
-SOURCES = ["capi.hip", "syrk.hip", "syrk_split.hip", "skinny.hip", "rr.hip", "oja.hip", "project.hip"]
+SOURCES = ["capi.hip", "syrk.hip", "syrk_split.hip", "skinny.hip", "rr.hip", "oja.hip", "project.hip",
+           "sweep.hip"]
 HEADERS = ["deig_internal.hpp", os.path.join("..", "..", "include", "deig.h")]
 ARCH = os.environ.get("DEIG_OFFLOAD_ARCH", "gfx950")
 

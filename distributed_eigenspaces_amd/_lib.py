@@ -24,6 +24,10 @@ DEIG_SYRK_AUTO = 0
 DEIG_SYRK_SPLIT3 = 1
 DEIG_SYRK_FP32 = 2
 SYRK_ALGOS = {"auto": DEIG_SYRK_AUTO, "split3": DEIG_SYRK_SPLIT3, "fp32": DEIG_SYRK_FP32}
+DEIG_SWEEP_AUTO = 0
+DEIG_SWEEP_SPLIT3 = 1
+DEIG_SWEEP_FP32 = 2
+SWEEP_ALGOS = {"auto": DEIG_SWEEP_AUTO, "split3": DEIG_SWEEP_SPLIT3, "fp32": DEIG_SWEEP_FP32}
 
 _c_i64 = ctypes.c_int64
 _c_sz = ctypes.c_size_t
@@ -54,6 +58,12 @@ SIGNATURES = {
     "deig_oja_step_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, ctypes.c_float, _fp,
                                          ctypes.c_int, _c_i64, _vp, _c_sz, _vp]),
     "deig_oja_workspace": (_c_sz, [_c_i64, _c_i64, ctypes.c_int]),
+    "deig_oja_steps_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_float,
+                                          _fp, ctypes.c_int, _c_i64, ctypes.c_int, _vp, _c_sz,
+                                          _vp]),
+    "deig_sym_apply_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _fp, ctypes.c_int, _c_i64, _fp,
+                                          _c_i64, ctypes.c_float, ctypes.c_int, _vp, _c_sz, _vp]),
+    "deig_sym_apply_workspace": (_c_sz, [_c_i64, ctypes.c_int, ctypes.c_int]),
     "deig_project_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, _fp, ctypes.c_int, _c_i64,
                                         _fp, _c_i64, _vp, _c_sz, _vp]),
     "deig_project_workspace": (_c_sz, [_c_i64, _c_i64, ctypes.c_int]),

@@ -64,7 +64,20 @@ struct SolverWs {
   float* Zt;
   float* slab;
   size_t slab_bytes;
+  void* sweep_ws;  // split-bf16 sweep (explicit S only)
+  size_t sweep_bytes;
 };
+
+// Sweep algorithm of the explicit-matrix solver: DEIG_SWEEP_ALGO=fp32 selects the
+// f32 MFMA skinny kernel, anything else the split-bf16 sweep.
+int sweep_algo_default() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DEIG_SWEEP_ALGO");
+    v = (e && strcmp(e, "fp32") == 0) ? DEIG_SWEEP_FP32 : DEIG_SWEEP_SPLIT3;
+  }
+  return v;
+}
 
 SolverWs carve_solver(void* ws, size_t cap, int64_t d, int k, int p, int64_t mk, size_t* total) {
   Carve c(ws, cap);
@@ -92,6 +105,12 @@ SolverWs carve_solver(void* ws, size_t cap, int64_t d, int k, int p, int64_t mk,
   }
   w.slab = c.take<float>(sb / sizeof(float) + 4);
   w.slab_bytes = sb;
+  w.sweep_ws = nullptr;
+  w.sweep_bytes = 0;
+  if (mk == 0 && sweep_algo_default() == DEIG_SWEEP_SPLIT3) {
+    w.sweep_bytes = sweep_workspace_bytes(d, p);
+    w.sweep_ws = c.take<char>(w.sweep_bytes);
+  }
   *total = c.off;
   return w;
 }
@@ -100,9 +119,12 @@ int apply_op(const Operator& op, const SolverWs& w, int64_t d, int p, hipStream_
   float* Q = w.rr.Z;
   float* Y = w.rr.Z + p;
   const int64_t ld = 2 * p;
-  if (!op.implicit)
+  if (!op.implicit) {
+    if (w.sweep_ws)
+      return sweep_launch(op.S, d, op.lds, Q, p, ld, Y, ld, 1.f, w.sweep_ws, w.sweep_bytes, st);
     return skinny_launch(true, op.S, op.lds, Q, ld, Y, ld, d, p, d, 1.f, 0.f, w.slab,
                          w.slab_bytes, st);
+  }
   int rc = skinny_launch(false, op.Wt, op.ldw, Q, ld, w.Zt, p, op.mk, p, d, 1.f, 0.f, w.slab,
                          w.slab_bytes, st);
   if (rc) return rc;
@@ -289,7 +311,33 @@ int deig_projavg_topk_f32(const float* Wt, int64_t d, int64_t mk, int64_t ldw, f
                ws, ws_bytes, (hipStream_t)stream);
 }
 
+size_t deig_sym_apply_workspace(int64_t d, int p, int algo) {
+  if (algo == DEIG_SWEEP_FP32) return skinny_workspace_bytes(d, p, d);
+  return sweep_workspace_bytes(d, p);
+}
+
+int deig_sym_apply_f32(const float* S, int64_t d, int64_t lds, const float* Q, int p,
+                       int64_t ldq, float* Y, int64_t ldy, float alpha, int algo, void* ws,
+                       size_t ws_bytes, void* stream) {
+  g_err[0] = 0;
+  if (algo == DEIG_SWEEP_FP32)
+    return skinny_launch(true, S, lds, Q, ldq, Y, ldy, d, p, d, alpha, 0.f,
+                         static_cast<float*>(ws), ws_bytes, (hipStream_t)stream);
+  if (algo != DEIG_SWEEP_AUTO && algo != DEIG_SWEEP_SPLIT3)
+    return fail(DEIG_EINVAL, "sym_apply: unknown algorithm %d", algo);
+  return sweep_launch(S, d, lds, Q, p, ldq, Y, ldy, alpha, ws, ws_bytes, (hipStream_t)stream);
+}
+
 size_t deig_oja_workspace(int64_t b, int64_t d, int k) { return oja_workspace_bytes(b, d, k); }
+
+int deig_oja_steps_f32(const float* X, int64_t nb, int64_t b, int64_t d, int64_t ldx, float eta,
+                       float* V, int k, int64_t ldv, int orth_every, void* ws, size_t ws_bytes,
+                       void* stream) {
+  g_err[0] = 0;
+  if (!X || !V || !aligned16(X)) return fail(DEIG_EINVAL, "oja: X must be 16-byte aligned");
+  return oja_steps_launch(X, nb, b, d, ldx, eta, V, k, ldv, orth_every, ws, ws_bytes,
+                          (hipStream_t)stream);
+}
 
 int deig_oja_step_f32(const float* Xb, int64_t b, int64_t d, int64_t ldx, float eta, float* V,
                       int k, int64_t ldv, void* ws, size_t ws_bytes, void* stream) {

@@ -73,6 +73,12 @@ int skinny_launch(bool trans_a, const float* A, int64_t lda, const float* B, int
                   float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha,
                   float beta, float* slab, size_t slab_bytes, hipStream_t stream);
 
+// Split-bf16 symmetric sweep (sweep.hip): Y = alpha * S Q, S symmetric d x d
+// row-major, Q d x p (ldq), Y d x p (ldy), p % 16 == 0, p <= 128.
+size_t sweep_workspace_bytes(int64_t d, int p);
+int sweep_launch(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
+                 float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st);
+
 // Rayleigh-Ritz pieces (rr.hip).
 struct RRBuffers {
   float* Z;          // d x 2p row-major: [Q | Y]
@@ -97,6 +103,9 @@ int rr_update_launch(const RRBuffers& b, int64_t d, int p, int k, float* V, int6
 size_t oja_workspace_bytes(int64_t b, int64_t d, int k);
 int oja_launch(const float* Xb, int64_t b, int64_t d, int64_t ldx, float eta, float* V,
                int k, int64_t ldv, void* ws, size_t ws_bytes, hipStream_t stream);
+int oja_steps_launch(const float* X, int64_t nb, int64_t b, int64_t d, int64_t ldx, float eta,
+                     float* V, int k, int64_t ldv, int orth_every, void* ws, size_t ws_bytes,
+                     hipStream_t stream);
 
 // Projection Y = X W (project.hip).
 size_t project_workspace_bytes(int64_t n, int64_t d, int k);

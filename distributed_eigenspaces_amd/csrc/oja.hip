@@ -1,8 +1,8 @@
-// Mini-batch Oja step for the online / streaming variant (BASELINE.json config 4):
+// Mini-batch Oja steps for the online / streaming variant (BASELINE.json config 4):
 //   V <- orth(V + eta/b * Xb^T (Xb V)),   orth = Cholesky-QR2.
 // Not present in the reference (parity unpinned; judged by sin(theta) against
-// the one-shot float64 oracle).  Xb is read twice (Xb V and Xb^T T), each pass a
-// skinny GEMM at ~k/2 flop/B (HBM-bound for k <= 32).
+// the one-shot float64 oracle and ref_cpu.oja_epoch).  Xb is read twice (Xb V
+// and Xb^T T), each pass a skinny GEMM at ~k/2 flop/B (HBM-bound for k <= 32).
 #include "deig_internal.hpp"
 
 namespace deig {
@@ -99,36 +99,10 @@ OjaWs carve_oja(void* ws, size_t cap, int64_t b, int64_t d, int kp, size_t* tota
   return o;
 }
 
-}  // namespace
-
-size_t oja_workspace_bytes(int64_t b, int64_t d, int k) {
-  const int kp = (int)cdiv(k, 16) * 16;
-  size_t total = 0;
-  carve_oja(nullptr, 0, b, d, kp, &total);
-  return total;
-}
-
-int oja_launch(const float* Xb, int64_t b, int64_t d, int64_t ldx, float eta, float* V, int k,
-               int64_t ldv, void* ws, size_t ws_bytes, hipStream_t st) {
-  DEIG_REQUIRE(b >= 1 && d >= 4 && d % 4 == 0, "oja: need b >= 1 and d %% 4 == 0");
-  DEIG_REQUIRE(k >= 1 && k <= 64 && k <= d, "oja: need 1 <= k <= min(64, d)");
-  DEIG_REQUIRE(ldx >= d && ldx % 4 == 0 && ldv >= d, "oja: bad leading dims");
-  const int kp = (int)cdiv(k, 16) * 16;
-  size_t total = 0;
-  OjaWs o = carve_oja(ws, ws_bytes, b, d, kp, &total);
-  if (!ws || total > ws_bytes) return fail(DEIG_EWORKSPACE, "oja: workspace %zu < %zu", ws_bytes, total);
+// Cholesky-QR2 of the row-padded d x kp basis in o.Vr (o.Vr2 is scratch); after
+// the two passes (two buffer swaps) the result is back in o.Vr.
+int cholqr2(const OjaWs& o, int64_t d, int k, int kp, hipStream_t st) {
   int rc;
-  hipLaunchKernelGGL(col_to_rowpad, dim3((unsigned)cdiv(d * kp, 256)), dim3(256), 0, st, V, ldv, d,
-                     k, kp, o.Vr);
-  DEIG_HIP_CHECK(hipGetLastError());
-  // T = Xb V
-  if ((rc = skinny_launch(false, Xb, ldx, o.Vr, kp, o.T, kp, b, kp, d, 1.f, 0.f, o.slab,
-                          o.slab_bytes, st)))
-    return rc;
-  // V += eta/b * Xb^T T
-  if ((rc = skinny_launch(true, Xb, ldx, o.T, kp, o.Vr, kp, d, kp, b, eta / (float)b, 1.f, o.slab,
-                          o.slab_bytes, st)))
-    return rc;
   float* cur = o.Vr;
   float* nxt = o.Vr2;
   for (int pass = 0; pass < 2; ++pass) {
@@ -144,10 +118,64 @@ int oja_launch(const float* Xb, int64_t b, int64_t d, int64_t ldx, float eta, fl
     cur = nxt;
     nxt = t;
   }
-  hipLaunchKernelGGL(rowpad_to_col, dim3((unsigned)cdiv(d * k, 256)), dim3(256), 0, st, cur, d, k,
+  return DEIG_OK;
+}
+
+}  // namespace
+
+size_t oja_workspace_bytes(int64_t b, int64_t d, int k) {
+  const int kp = (int)cdiv(k, 16) * 16;
+  size_t total = 0;
+  carve_oja(nullptr, 0, b, d, kp, &total);
+  return total;
+}
+
+// nb consecutive batches of b rows (batch i starts at row i * b of X).  Each
+// batch applies V <- V + eta/b Xb^T (Xb V); the basis is re-orthonormalised
+// (CholQR2) every orth_every batches and after the last one.  The update is
+// linear in V and an orthonormalisation only right-multiplies V by an
+// invertible k x k factor, so the span after every batch equals the one of
+// per-batch orthonormalisation (ref_cpu.oja_epoch); deferring it only lets the
+// column norms grow by ~(1 + eta lambda_max)^orth_every in between.
+int oja_steps_launch(const float* X, int64_t nb, int64_t b, int64_t d, int64_t ldx, float eta,
+                     float* V, int k, int64_t ldv, int orth_every, void* ws, size_t ws_bytes,
+                     hipStream_t st) {
+  DEIG_REQUIRE(nb >= 1 && b >= 1 && d >= 4 && d % 4 == 0,
+               "oja: need nb >= 1, b >= 1 and d %% 4 == 0");
+  DEIG_REQUIRE(k >= 1 && k <= 64 && k <= d, "oja: need 1 <= k <= min(64, d)");
+  DEIG_REQUIRE(ldx >= d && ldx % 4 == 0 && ldv >= d, "oja: bad leading dims");
+  DEIG_REQUIRE(orth_every >= 1, "oja: orth_every must be >= 1");
+  const int kp = (int)cdiv(k, 16) * 16;
+  size_t total = 0;
+  OjaWs o = carve_oja(ws, ws_bytes, b, d, kp, &total);
+  if (!ws || total > ws_bytes)
+    return fail(DEIG_EWORKSPACE, "oja: workspace %zu < %zu", ws_bytes, total);
+  int rc;
+  hipLaunchKernelGGL(col_to_rowpad, dim3((unsigned)cdiv(d * kp, 256)), dim3(256), 0, st, V, ldv, d,
+                     k, kp, o.Vr);
+  DEIG_HIP_CHECK(hipGetLastError());
+  for (int64_t i = 0; i < nb; ++i) {
+    const float* Xb = X + i * b * ldx;
+    // T = Xb V
+    if ((rc = skinny_launch(false, Xb, ldx, o.Vr, kp, o.T, kp, b, kp, d, 1.f, 0.f, o.slab,
+                            o.slab_bytes, st)))
+      return rc;
+    // V += eta/b * Xb^T T
+    if ((rc = skinny_launch(true, Xb, ldx, o.T, kp, o.Vr, kp, d, kp, b, eta / (float)b, 1.f,
+                            o.slab, o.slab_bytes, st)))
+      return rc;
+    if ((i + 1) % orth_every == 0 || i + 1 == nb)
+      if ((rc = cholqr2(o, d, k, kp, st))) return rc;
+  }
+  hipLaunchKernelGGL(rowpad_to_col, dim3((unsigned)cdiv(d * k, 256)), dim3(256), 0, st, o.Vr, d, k,
                      kp, V, ldv);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
+}
+
+int oja_launch(const float* Xb, int64_t b, int64_t d, int64_t ldx, float eta, float* V, int k,
+               int64_t ldv, void* ws, size_t ws_bytes, hipStream_t st) {
+  return oja_steps_launch(Xb, 1, b, d, ldx, eta, V, k, ldv, 1, ws, ws_bytes, st);
 }
 
 }  // namespace deig

@@ -23,6 +23,7 @@ from . import _lib
 __all__ = [
     "sigma_hat", "topk_eigh", "projavg_topk", "oja_step", "default_subspace",
     "EigResult", "require_device_tensor", "project", "stack_bases", "gemm_skinny",
+    "oja_steps", "sym_apply",
 ]
 
 DEFAULT_TOL = 1e-6
@@ -298,6 +299,64 @@ def oja_step(Xb: torch.Tensor, V: torch.Tensor, eta: float) -> torch.Tensor:
                                  _stream(Xb.device))
     _lib.check(rc, "deig_oja_step_f32")
     return V
+
+
+def oja_steps(X: torch.Tensor, V: torch.Tensor, eta: float, batch: int,
+              orth_every: int = 8) -> torch.Tensor:
+    """In-place Oja over the consecutive row batches X[i*batch:(i+1)*batch] (config 4).
+
+    One C call for all batches (no host work in between); the basis is
+    re-orthonormalised every ``orth_every`` batches and at the end, which gives the
+    span of per-batch orthonormalisation (``oja_step`` in a loop) because the update
+    is linear in V.  Rows beyond the last full batch are ignored.  Returns V."""
+    X = _rowmajor_4(require_device_tensor(X, "oja_steps"), "X")
+    n, d = X.shape
+    b = int(batch)
+    nb = n // b if b > 0 else 0
+    if nb < 1:
+        raise ValueError(f"need at least one full batch of {batch} rows, got {n} rows")
+    if V.dim() != 2 or V.shape[0] != d or V.stride(0) != 1 or V.dtype != torch.float32 \
+            or V.device != X.device:
+        raise ValueError("V must be a (d, k) column-major float32 tensor on X's device")
+    k = V.shape[1]
+    L = _lib.lib()
+    with torch.cuda.device(X.device):
+        nbytes = L.deig_oja_workspace(b, d, k)
+        ws = _workspace(X.device, nbytes)
+        rc = L.deig_oja_steps_f32(X.data_ptr(), nb, b, d, X.stride(0), ctypes.c_float(eta),
+                                  V.data_ptr(), k, V.stride(1), int(orth_every), ws.data_ptr(),
+                                  nbytes, _stream(X.device))
+    _lib.check(rc, "deig_oja_steps_f32")
+    return V
+
+
+# ---------------------------------------------------------------- sweep
+def sym_apply(S: torch.Tensor, Q: torch.Tensor, algo: str = "auto", alpha: float = 1.0,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    """Y = alpha * S Q for symmetric S (d x d) and Q (d x p, p % 16 == 0, p <= 128):
+    one subspace-iteration sweep of ``topk_eigh`` (include/deig.h DEIG_SWEEP_*)."""
+    if algo not in _lib.SWEEP_ALGOS:
+        raise ValueError(f"algo must be one of {sorted(_lib.SWEEP_ALGOS)}, got {algo!r}")
+    S = require_device_tensor(S, "sym_apply")
+    Q = require_device_tensor(Q, "Q")
+    d = S.shape[0]
+    if S.dim() != 2 or S.shape[1] != d or Q.dim() != 2 or Q.shape[0] != d:
+        raise ValueError(f"shape mismatch: S {tuple(S.shape)}, Q {tuple(Q.shape)}")
+    p = Q.shape[1]
+    if d % 4 or S.stride(1) != 1 or S.stride(0) % 4 or S.data_ptr() % 16:
+        raise ValueError("S must be row-major with d % 4 == 0 and a 16-byte aligned, %4 stride")
+    Q = Q.contiguous()
+    Y = out if out is not None else torch.empty((d, p), dtype=torch.float32, device=S.device)
+    code = _lib.SWEEP_ALGOS[algo]
+    L = _lib.lib()
+    with torch.cuda.device(S.device):
+        nbytes = L.deig_sym_apply_workspace(d, p, code)
+        ws = _workspace(S.device, nbytes)
+        rc = L.deig_sym_apply_f32(S.data_ptr(), d, S.stride(0), Q.data_ptr(), p, Q.stride(0),
+                                  Y.data_ptr(), Y.stride(0), ctypes.c_float(alpha), code,
+                                  ws.data_ptr(), nbytes, _stream(S.device))
+    _lib.check(rc, "deig_sym_apply_f32")
+    return Y
 
 
 # ---------------------------------------------------------------- projection

@@ -62,7 +62,7 @@ class StreamingOja:
     """
 
     def __init__(self, V0: torch.Tensor, eta: float, agg_every: int = 64, server_rank: int = 0,
-                 group=None, step_fn=None, server_fn=None):
+                 group=None, step_fn=None, server_fn=None, block_fn=None):
         d, k = V0.shape
         self.k = int(k)
         self.V = torch.empty((k, d), dtype=torch.float32, device=V0.device).t()
@@ -73,6 +73,7 @@ class StreamingOja:
         self.group = group
         self.step_fn = step_fn or linalg.oja_step
         self.server_fn = server_fn or _gpu_server
+        self.block_fn = block_fn or linalg.oja_steps
         self.batches_seen = 0
         self.aggregations = 0
 
@@ -82,6 +83,23 @@ class StreamingOja:
         self.batches_seen += 1
         if self.agg_every > 0 and self.batches_seen % self.agg_every == 0:
             self.aggregate()
+        return self.V
+
+    def partial_fit_block(self, X: torch.Tensor, batch: int, orth_every: int = 8) -> torch.Tensor:
+        """Oja steps over the consecutive row batches of X (rows beyond the last full
+        batch are ignored), one ``linalg.oja_steps`` call per run of batches between
+        two aggregation points; aggregates exactly where ``partial_fit`` would."""
+        nb = X.shape[0] // int(batch)
+        i = 0
+        while i < nb:
+            seg = nb - i
+            if self.agg_every > 0:
+                seg = min(seg, self.agg_every - self.batches_seen % self.agg_every)
+            self.block_fn(X[i * batch:(i + seg) * batch], self.V, self.eta, batch, orth_every)
+            self.batches_seen += seg
+            i += seg
+            if self.agg_every > 0 and self.batches_seen % self.agg_every == 0:
+                self.aggregate()
         return self.V
 
     def aggregate(self) -> torch.Tensor:

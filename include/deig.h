@@ -74,6 +74,26 @@ size_t deig_syrk_workspace_ex(int64_t n, int64_t d, int algo);
 /* Subspace size the solvers use for a given k when the caller passes p <= 0. */
 int deig_default_subspace(int64_t d, int k);
 
+/* Sweep algorithms for the symmetric S*Q product of the eigensolver:
+ *  DEIG_SWEEP_SPLIT3: S rows and Q split into bf16 hi + lo in registers, 3 bf16 MFMA
+ *    products per fp32 product, fp32 accumulation - HBM-bound on the 4 d^2 bytes of
+ *    S for every p <= 128 (per-product error ~2^-18 relative, zero-mean);
+ *  DEIG_SWEEP_FP32: f32 MFMA skinny kernel (exact fp32 fma chain, f32-MFMA-bound
+ *    above p ~ 40);
+ *  DEIG_SWEEP_AUTO: SPLIT3.  deig_topk_sym_f32 uses AUTO unless the environment sets
+ *    DEIG_SWEEP_ALGO=fp32. */
+#define DEIG_SWEEP_AUTO 0
+#define DEIG_SWEEP_SPLIT3 1
+#define DEIG_SWEEP_FP32 2
+
+/* One subspace-iteration sweep Y = alpha * S Q  (S symmetric d x d row-major, lds;
+ * Q d x p row-major, ldq; Y d x p row-major, ldy; p % 16 == 0, 16 <= p <= 128).
+ * The S*Q product inside deig_topk_sym_f32, exposed for measurement and reuse. */
+int deig_sym_apply_f32(const float* S, int64_t d, int64_t lds, const float* Q, int p,
+                       int64_t ldq, float* Y, int64_t ldy, float alpha, int algo, void* ws,
+                       size_t ws_bytes, void* stream);
+size_t deig_sym_apply_workspace(int64_t d, int p, int algo);
+
 /* Top-k eigenpairs of a dense symmetric S (d x d, row-major, lds), ascending.
  * Replaces Node.top_k_eigenvectors  distributed.py:22-29
  * (scipy.linalg.eigh(S, eigvals=(d-k, d-1))[1]  ->  LAPACK dsyevr), plus the
@@ -112,6 +132,15 @@ int deig_oja_step_f32(const float* Xb, int64_t b, int64_t d, int64_t ldx, float 
                       float* V, int k, int64_t ldv, void* ws, size_t ws_bytes,
                       void* stream);
 size_t deig_oja_workspace(int64_t b, int64_t d, int k);
+
+/* nb consecutive Oja steps over the batches X[i*b:(i+1)*b] (X: (nb*b) x d row-major,
+ * ldx), V updated in place.  The basis is re-orthonormalised (CholQR2) every
+ * orth_every batches and after the last one: the update is linear in V, so the
+ * span after each batch equals that of per-batch orthonormalisation.  Same
+ * workspace as deig_oja_step_f32 (deig_oja_workspace(b, d, k)). */
+int deig_oja_steps_f32(const float* X, int64_t nb, int64_t b, int64_t d, int64_t ldx, float eta,
+                       float* V, int k, int64_t ldv, int orth_every, void* ws, size_t ws_bytes,
+                       void* stream);
 
 /* Projection onto an estimated eigenspace: Y = X W.
  * Replaces the notebook's  online_distributed_PCA = lambda X: X @ matrix_w

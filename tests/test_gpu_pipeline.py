@@ -212,3 +212,43 @@ def test_full_size_worker_recovers_planted_subspace(cuda):
     V = r.V.double()
     R = S.double() @ V - V * r.evals.double()[None, :]
     assert float(R.norm(dim=0).max() / ev[-1]) < 1e-5
+
+
+def test_oja_steps_deferred_orthonormalisation_matches_oracle(cuda):
+    """oja_steps (one C call, CholQR2 every orth_every batches) spans the same
+    subspace as per-batch orthonormalisation (ref_cpu.oja_epoch); parity
+    unpinned w.r.t. the reference (no Oja there)."""
+    import distributed_eigenspaces_amd as de
+    from distributed_eigenspaces_amd import synthetic
+    d, k, b, steps, eta = 512, 8, 2048, 16, 0.5
+    U = synthetic.planted_basis(d, k, seed=3, device=cuda)
+    X = synthetic.spiked_samples(steps * b + 100, U, seed=4)  # + a partial batch (ignored)
+    V0 = torch.linalg.qr(torch.randn(d, k, device=cuda, dtype=torch.float64))[0]
+    Vr = ref_cpu.oja_epoch(X[:steps * b].double().cpu().numpy(), V0.cpu().numpy(), eta, b)
+    for orth_every in (1, 3, 8):
+        V = V0.float().t().contiguous().t()
+        de.oja_steps(X, V, eta, b, orth_every=orth_every)
+        Vg = V.cpu().numpy()
+        np.testing.assert_allclose(Vg.T @ Vg, np.eye(k), atol=1e-5)
+        assert ref_cpu.projector_distance(Vg, Vr) <= P_TOL, orth_every
+
+
+def test_streaming_oja_single_rank_matches_oracle(cuda):
+    """StreamingOja on one rank (aggregation = server solve of its own basis)
+    == ref_cpu.oja_stream with R = 1; block and per-batch feeding agree."""
+    from distributed_eigenspaces_amd import synthetic
+    from distributed_eigenspaces_amd.streaming import StreamingOja
+    d, k, b, nb, eta, agg = 256, 6, 1024, 10, 0.3, 4
+    U = synthetic.planted_basis(d, k, seed=5, device=cuda)
+    X = synthetic.spiked_samples(nb * b, U, seed=6)
+    V0 = torch.linalg.qr(torch.randn(d, k, device=cuda, dtype=torch.float64))[0].float()
+    a = StreamingOja(V0, eta=eta, agg_every=agg)
+    for i in range(nb):
+        a.partial_fit(X[i * b:(i + 1) * b])
+    c = StreamingOja(V0, eta=eta, agg_every=agg)
+    c.partial_fit_block(X, b)
+    assert a.aggregations == c.aggregations == nb // agg
+    batches = [X[i * b:(i + 1) * b].double().cpu().numpy() for i in range(nb)]
+    ref = ref_cpu.oja_stream([batches], V0.double().cpu().numpy(), eta, agg)
+    assert ref_cpu.projector_distance(a.V.cpu().numpy(), ref) <= P_TOL
+    assert ref_cpu.projector_distance(c.V.cpu().numpy(), ref) <= P_TOL
