@@ -155,15 +155,16 @@ def sweep_roofline(de, S: torch.Tensor, p: int, stream) -> dict:
     byt, fl = 4.0 * d * d, 2.0 * d * d * p
     out = {"d": d, "p": p, "bound": "hbm", "algorithmic": "4 d^2 bytes (S read once), 2 d^2 p flop",
            "peak_GBs": HBM_PEAK / 1e9}
-    for algo in ("split3", "fp32"):
+    for algo in ("bf16x6", "fp32"):
         ms = time_events(lambda: de.sym_apply(S, Q, algo=algo, out=Y), 20, stream)
         t = ms * 1e-3
-        t_min = max(byt / HBM_PEAK, fl / (BF16_MFMA_PEAK / 3 if algo == "split3" else FP32_MFMA_PEAK))
+        t_min = max(byt / HBM_PEAK, fl / (BF16_MFMA_PEAK / 6 if algo == "bf16x6" else FP32_MFMA_PEAK))
         out[algo] = {"us": ms * 1e3, "hbm_GBs": byt / t / 1e9, "hbm_frac": byt / t / HBM_PEAK,
                      "fp32_equiv_tflops": fl / t / 1e12, "attainable_frac": t_min / t}
-    out["kernel"] = ("split3: split_q_kernel + sweep_kernel (+ sweep_reduce_kernel), bf16 MFMA "
-                     "16x16x32 on split S rows and Q; fp32: skinny_kernel<T> f32 MFMA 16x16x4")
-    out["solver_uses"] = "split3"
+    out["kernel"] = ("bf16x6: split_q_kernel + sweep_kernel (+ sweep_reduce_kernel), 6 bf16 MFMA "
+                     "16x16x32 products of 3-piece split S rows and Q; fp32: skinny_kernel<T> "
+                     "f32 MFMA 16x16x4")
+    out["solver_uses"] = "bf16x6"
     return out
 
 

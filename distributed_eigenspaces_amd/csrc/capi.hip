@@ -64,17 +64,17 @@ struct SolverWs {
   float* Zt;
   float* slab;
   size_t slab_bytes;
-  void* sweep_ws;  // split-bf16 sweep (explicit S only)
+  void* sweep_ws;  // bf16x6 sweep (explicit S only)
   size_t sweep_bytes;
 };
 
 // Sweep algorithm of the explicit-matrix solver: DEIG_SWEEP_ALGO=fp32 selects the
-// f32 MFMA skinny kernel, anything else the split-bf16 sweep.
+// f32 MFMA skinny kernel, anything else the bf16x6 sweep (sweep.hip).
 int sweep_algo_default() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("DEIG_SWEEP_ALGO");
-    v = (e && strcmp(e, "fp32") == 0) ? DEIG_SWEEP_FP32 : DEIG_SWEEP_SPLIT3;
+    v = (e && strcmp(e, "fp32") == 0) ? DEIG_SWEEP_FP32 : DEIG_SWEEP_BF16X6;
   }
   return v;
 }
@@ -107,7 +107,7 @@ SolverWs carve_solver(void* ws, size_t cap, int64_t d, int k, int p, int64_t mk,
   w.slab_bytes = sb;
   w.sweep_ws = nullptr;
   w.sweep_bytes = 0;
-  if (mk == 0 && sweep_algo_default() == DEIG_SWEEP_SPLIT3) {
+  if (mk == 0 && sweep_algo_default() == DEIG_SWEEP_BF16X6) {
     w.sweep_bytes = sweep_workspace_bytes(d, p);
     w.sweep_ws = c.take<char>(w.sweep_bytes);
   }
@@ -168,10 +168,8 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
   for (it = 0; it < max_sweeps; ++it) {
     if ((rc = apply_op(op, w, d, p, st))) return rc;
     if (it > 0 && ++since_rr < rr_every && it + 1 < max_sweeps) {
-      // power step: Q <- Y (columns p..2p-1 of Z into columns 0..p-1)
-      DEIG_HIP_CHECK(hipMemcpy2DAsync(w.rr.Z, sizeof(float) * 2 * p, w.rr.Z + p,
-                                      sizeof(float) * 2 * p, sizeof(float) * p, d,
-                                      hipMemcpyDeviceToDevice, st));
+      // power step on the live Ritz columns of the last RR (Q_j <- Y_j / ||Y w_j||)
+      if ((rc = rr_power_launch(w.rr, d, p, st))) return rc;
       continue;
     }
     since_rr = 0;
@@ -188,7 +186,7 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
       fprintf(stderr, "[deig] d=%lld k=%d p=%d sweep %d resid %.3e chol_floor %d jacobi_sweeps %d rotations %d\n",
               (long long)d, k, p, it + 1, last, inf[0], inf[1], inf[2]);
     }
-    if (!(last == last)) {  // NaN
+    if (!(last == last) || last > 3.0e38f) {  // NaN / Inf
       if (sweeps_out) *sweeps_out = it + 1;
       if (resid_out) *resid_out = last;
       return fail(DEIG_EINVAL, "solver: non-finite residual (input contains NaN/Inf?)");
@@ -323,7 +321,7 @@ int deig_sym_apply_f32(const float* S, int64_t d, int64_t lds, const float* Q, i
   if (algo == DEIG_SWEEP_FP32)
     return skinny_launch(true, S, lds, Q, ldq, Y, ldy, d, p, d, alpha, 0.f,
                          static_cast<float*>(ws), ws_bytes, (hipStream_t)stream);
-  if (algo != DEIG_SWEEP_AUTO && algo != DEIG_SWEEP_SPLIT3)
+  if (algo != DEIG_SWEEP_AUTO && algo != DEIG_SWEEP_BF16X6)
     return fail(DEIG_EINVAL, "sym_apply: unknown algorithm %d", algo);
   return sweep_launch(S, d, lds, Q, p, ldq, Y, ldy, alpha, ws, ws_bytes, (hipStream_t)stream);
 }

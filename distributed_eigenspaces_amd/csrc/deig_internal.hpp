@@ -96,6 +96,7 @@ int rr_init_launch(float* Z, int64_t d, int p, const float* Q0, int k0, int64_t 
                    uint64_t seed, hipStream_t stream);
 int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream);
 int rr_update_blocks(int64_t d);
+int rr_power_launch(const RRBuffers& b, int64_t d, int p, hipStream_t stream);
 int rr_update_launch(const RRBuffers& b, int64_t d, int p, int k, float* V, int64_t ldv,
                      float* evals, hipStream_t stream);
 

@@ -422,11 +422,34 @@ __global__ __launch_bounds__(256) void rr_finish_kernel(const float* __restrict_
       resid[j] = rel;
       evals[k - 1 - j] = lam[j];
     }
-    m = fmaxf(m, rel);
+    m = (rel == rel) ? fmaxf(m, rel) : rel;  // NaN propagates (fmaxf would drop it)
   }
   if (lane == 0) mx[wave] = m;
   __syncthreads();
-  if (threadIdx.x == 0) resid[k] = fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3]));
+  if (threadIdx.x == 0) {
+    float r = mx[0];
+    for (int w = 1; w < 4; ++w) r = (r == r && mx[w] == mx[w]) ? fmaxf(r, mx[w]) : __int_as_float(0x7fc00000);
+    resid[k] = r;
+  }
+}
+
+// Power step between two Rayleigh-Ritz sweeps: Q_j <- Y_j * cs_j for the live
+// Ritz columns of the last RR (cs_j = 1 / ||Y w_j||, so the columns stay ~unit
+// norm) whose Ritz value is within 10x of the largest.  Dead columns (cs_j == 0:
+// null directions of a rank-deficient operator) keep Q_j, as rr_update treats
+// them, and so do weak columns: an extra power step multiplies their
+// contamination by the dominant directions by |lambda_0 / lambda_j| before the
+// next RR re-orthogonalises, which for a wide spectrum (the projector average:
+// 1 vs << 1) makes the basis numerically dependent.
+__global__ __launch_bounds__(256) void rr_power_kernel(float* __restrict__ Z, int64_t d, int p,
+                                                       const float* __restrict__ cs,
+                                                       const float* __restrict__ lam) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= d * p) return;
+  const int64_t r = idx / p;
+  const int j = (int)(idx - r * p);
+  const float c = cs[j];
+  if (c > 0.f && fabsf(lam[j]) >= 0.1f * fabsf(lam[0])) Z[r * 2 * p + j] = Z[r * 2 * p + p + j] * c;
 }
 
 size_t rr_small_shm(int p) {
@@ -456,6 +479,13 @@ int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream) {
   }
   hipLaunchKernelGGL(rr_small_kernel, dim3(1), dim3(RT), shm, stream, b.C, p, b.W, b.lam, b.cs,
                      b.info, 30);
+  DEIG_HIP_CHECK(hipGetLastError());
+  return DEIG_OK;
+}
+
+int rr_power_launch(const RRBuffers& b, int64_t d, int p, hipStream_t stream) {
+  hipLaunchKernelGGL(rr_power_kernel, dim3((unsigned)cdiv(d * p, 256)), dim3(256), 0, stream, b.Z,
+                     d, p, b.cs, b.lam);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }

@@ -3,12 +3,17 @@
 // The S*Q product of every sweep of the eigensolver that replaces LAPACK dsyevr
 // in Node.top_k_eigenvectors (distributed.py:22-29).  S (d x d fp32, symmetric,
 // row-major) is streamed from HBM once per sweep and split in registers into
-// bf16 hi + lo (x = hi + lo + O(2^-18 |x|)); Q (d x p fp32) is split once per
-// sweep into an image in MFMA B-operand order (split_q_kernel).  Each product
-// is formed from three bf16 MFMA products hi*hi + hi*lo + lo*hi accumulated in
-// fp32 (the scheme of the covariance kernel, syrk_split.hip), which takes the
-// sweep from the f32-MFMA roof (2 d^2 p flop at 157 TF/s) under the HBM roof
-// (4 d^2 bytes of S at 8 TB/s) for every p <= 128.
+// three bf16 pieces x = h + m + l (|x - h - m - l| <= 2^-27 |x|); Q (d x p fp32)
+// is split the same way once per sweep into an image in MFMA B-operand order
+// (split_q_kernel).  Each product is formed from the six bf16 MFMA products
+// h h + h m + m h + h l + l h + m m (every term down to 2^-16 |ab|), accumulated
+// in fp32: the dropped terms are <= ~2^-23 |ab|, i.e. fp32-grade products.  Two
+// pieces (the covariance kernel's split3) are not enough here: their ~2^-17
+// representation error survives in the null-space images S q ~ 0 and the
+// residual test of the solver, while the covariance averages it out over n.
+// Six bf16 MFMAs cost 6/16 of one f32 MFMA, so the sweep stays under the HBM
+// roof (4 d^2 bytes of S at 8 TB/s) instead of the f32-MFMA roof (2 d^2 p flop
+// at 157 TF/s) for p <= 128.
 //
 // Y[m][:] = sum_k S[m][k] Q[k][:]  (S = S^T, so ROWS of S are read, contiguous
 // along k).  v_mfma_f32_16x16x32_bf16: lane l holds A[m = l%16][k = 8(l/16)..+7]
@@ -37,16 +42,24 @@ __device__ __forceinline__ uint32_t rne_bf16(float x) {
   return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
 }
 
-// 8 consecutive fp32 values -> packed bf16 hi and lo MFMA operands.
-__device__ __forceinline__ void split8(const f32x4& a, const f32x4& b, u32x4& hi, u32x4& lo) {
+// 8 consecutive fp32 values -> packed bf16 h, m, l MFMA operands (x = h + m + l).
+__device__ __forceinline__ void split8(const f32x4& a, const f32x4& b, u32x4& hi, u32x4& mi,
+                                       u32x4& lo) {
   const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const uint32_t h0 = rne_bf16(v[2 * q]), h1 = rne_bf16(v[2 * q + 1]);
-    const uint32_t l0 = rne_bf16(v[2 * q] - __uint_as_float(h0 << 16));
-    const uint32_t l1 = rne_bf16(v[2 * q + 1] - __uint_as_float(h1 << 16));
-    hi[q] = h0 | (h1 << 16);
-    lo[q] = l0 | (l1 << 16);
+    uint32_t h[2], m[2], l[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float x = v[2 * q + e];
+      h[e] = rne_bf16(x);
+      const float r1 = x - __uint_as_float(h[e] << 16);
+      m[e] = rne_bf16(r1);
+      l[e] = rne_bf16(r1 - __uint_as_float(m[e] << 16));
+    }
+    hi[q] = h[0] | (h[1] << 16);
+    mi[q] = m[0] | (m[1] << 16);
+    lo[q] = l[0] | (l[1] << 16);
   }
 }
 
@@ -55,7 +68,7 @@ __device__ __forceinline__ f32x4 mfma16(const u32x4& a, const u32x4& b, const f3
                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
 
-// Q (d x p, row stride ldq) -> image [k-group g = k/32][n-block j][hi|lo][lane][16 B],
+// Q (d x p, row stride ldq) -> image [k-group g = k/32][n-block j][h|m|l][lane][16 B],
 // lane l of (g, j) holding Q[32 g + 8 (l/16) + e][16 j + l%16], e = 0..7; k-groups
 // beyond d are zeros.  One thread per (g, j, lane).
 __global__ __launch_bounds__(256) void split_q_kernel(const float* __restrict__ Q, int64_t ldq,
@@ -72,10 +85,11 @@ __global__ __launch_bounds__(256) void split_q_kernel(const float* __restrict__ 
   float v[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = (k0 + e < d) ? Q[(k0 + e) * ldq + n] : 0.f;
-  u32x4 hi, lo;
-  split8(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, hi, lo);
-  QS[(t * 2 + 0) * 64 + lane] = hi;
-  QS[(t * 2 + 1) * 64 + lane] = lo;
+  u32x4 hi, mi, lo;
+  split8(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, hi, mi, lo);
+  QS[(t * 3 + 0) * 64 + lane] = hi;
+  QS[(t * 3 + 1) * 64 + lane] = mi;
+  QS[(t * 3 + 2) * 64 + lane] = lo;
 }
 
 template <int NB>
@@ -84,7 +98,7 @@ __global__ __launch_bounds__(SW_THR) void sweep_kernel(const float* __restrict__
                                                        int64_t nsteps, float* __restrict__ Y,
                                                        int64_t ldy, float alpha,
                                                        float* __restrict__ part) {
-  constexpr int BV = 2 * NB * 2 * 64;  // 16-B units of one Q stage (2 k-groups)
+  constexpr int BV = 2 * NB * 3 * 64;  // 16-B units of one Q stage (2 k-groups)
   constexpr int BPT = (BV + SW_THR - 1) / SW_THR;
   __shared__ u32x4 Bs[2][BV];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -146,11 +160,12 @@ __global__ __launch_bounds__(SW_THR) void sweep_kernel(const float* __restrict__
     int cur = 0;
     for (int64_t step = c0; step < c1; ++step) {
       const bool more = step + 1 < c1;
-      u32x4 ah[2][2], al[2][2];
+      u32x4 ah[2][2], am[2][2], al[2][2];
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
-        for (int g = 0; g < 2; ++g) split8(ra[mb][g][0], ra[mb][g][1], ah[mb][g], al[mb][g]);
+        for (int g = 0; g < 2; ++g)
+          split8(ra[mb][g][0], ra[mb][g][1], ah[mb][g], am[mb][g], al[mb][g]);
       if (more) {
         load_a(step + 1);
         load_q(step + 1);
@@ -159,13 +174,17 @@ __global__ __launch_bounds__(SW_THR) void sweep_kernel(const float* __restrict__
       for (int g = 0; g < 2; ++g)
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
-          const u32x4 bh = Bs[cur][((g * NB + j) * 2 + 0) * 64 + lane];
-          const u32x4 bl = Bs[cur][((g * NB + j) * 2 + 1) * 64 + lane];
+          const u32x4 bh = Bs[cur][((g * NB + j) * 3 + 0) * 64 + lane];
+          const u32x4 bm = Bs[cur][((g * NB + j) * 3 + 1) * 64 + lane];
+          const u32x4 bl = Bs[cur][((g * NB + j) * 3 + 2) * 64 + lane];
 #pragma unroll
-          for (int mb = 0; mb < 2; ++mb) {
-            acc[mb][j] = mfma16(ah[mb][g], bh, acc[mb][j]);
+          for (int mb = 0; mb < 2; ++mb) {  // small terms first
+            acc[mb][j] = mfma16(am[mb][g], bm, acc[mb][j]);
             acc[mb][j] = mfma16(ah[mb][g], bl, acc[mb][j]);
             acc[mb][j] = mfma16(al[mb][g], bh, acc[mb][j]);
+            acc[mb][j] = mfma16(ah[mb][g], bm, acc[mb][j]);
+            acc[mb][j] = mfma16(am[mb][g], bh, acc[mb][j]);
+            acc[mb][j] = mfma16(ah[mb][g], bh, acc[mb][j]);
           }
         }
       if (more) store_q(cur ^ 1);
@@ -223,7 +242,8 @@ int sweep_ks(int64_t d) {
   return (int)ks;
 }
 
-size_t qs_bytes(int64_t d, int p) { return (size_t)cdiv(d, SW_KS) * SW_KS * p * sizeof(float); }
+// Q image: 3 bf16 pieces per value
+size_t qs_bytes(int64_t d, int p) { return (size_t)cdiv(d, SW_KS) * SW_KS * p * 6; }
 
 template <int NB>
 void launch_nb(dim3 grid, hipStream_t st, const float* S, int64_t lds, int64_t d, const u32x4* QS,

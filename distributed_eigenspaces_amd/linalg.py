@@ -334,7 +334,8 @@ def oja_steps(X: torch.Tensor, V: torch.Tensor, eta: float, batch: int,
 def sym_apply(S: torch.Tensor, Q: torch.Tensor, algo: str = "auto", alpha: float = 1.0,
               out: torch.Tensor | None = None) -> torch.Tensor:
     """Y = alpha * S Q for symmetric S (d x d) and Q (d x p, p % 16 == 0, p <= 128):
-    one subspace-iteration sweep of ``topk_eigh`` (include/deig.h DEIG_SWEEP_*)."""
+    one subspace-iteration sweep of ``topk_eigh`` (include/deig.h DEIG_SWEEP_*):
+    algo "bf16x6" (default via "auto") or "fp32"."""
     if algo not in _lib.SWEEP_ALGOS:
         raise ValueError(f"algo must be one of {sorted(_lib.SWEEP_ALGOS)}, got {algo!r}")
     S = require_device_tensor(S, "sym_apply")

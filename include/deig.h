@@ -75,15 +75,16 @@ size_t deig_syrk_workspace_ex(int64_t n, int64_t d, int algo);
 int deig_default_subspace(int64_t d, int k);
 
 /* Sweep algorithms for the symmetric S*Q product of the eigensolver:
- *  DEIG_SWEEP_SPLIT3: S rows and Q split into bf16 hi + lo in registers, 3 bf16 MFMA
- *    products per fp32 product, fp32 accumulation - HBM-bound on the 4 d^2 bytes of
- *    S for every p <= 128 (per-product error ~2^-18 relative, zero-mean);
+ *  DEIG_SWEEP_BF16X6: S rows and Q split into three bf16 pieces in registers
+ *    (x = h + m + l), 6 bf16 MFMA products per fp32 product (every term down to
+ *    2^-16 |ab|), fp32 accumulation - fp32-grade products, HBM-bound on the 4 d^2
+ *    bytes of S for every p <= 128;
  *  DEIG_SWEEP_FP32: f32 MFMA skinny kernel (exact fp32 fma chain, f32-MFMA-bound
  *    above p ~ 40);
- *  DEIG_SWEEP_AUTO: SPLIT3.  deig_topk_sym_f32 uses AUTO unless the environment sets
- *    DEIG_SWEEP_ALGO=fp32. */
+ *  DEIG_SWEEP_AUTO: BF16X6.  deig_topk_sym_f32 uses AUTO unless the environment
+ *    sets DEIG_SWEEP_ALGO=fp32. */
 #define DEIG_SWEEP_AUTO 0
-#define DEIG_SWEEP_SPLIT3 1
+#define DEIG_SWEEP_BF16X6 1
 #define DEIG_SWEEP_FP32 2
 
 /* One subspace-iteration sweep Y = alpha * S Q  (S symmetric d x d row-major, lds;
