@@ -5,6 +5,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <math.h>
 
 #include "deig_internal.hpp"
 
@@ -156,7 +157,8 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
   // generalised RR copes with the non-orthonormal basis).  The single-workgroup
   // small solve is the latency-bound part of a sweep, so this divides its cost.
   static const int rr_every_env = getenv("DEIG_RR_EVERY") ? atoi(getenv("DEIG_RR_EVERY")) : 0;
-  const int rr_every = rr_every_env > 0 ? rr_every_env : 2;
+  const int rr_every = rr_every_env > 0 ? rr_every_env : 4;
+  const float tau = rr_every > 1 ? powf(0.1f, 1.0f / (float)(rr_every - 1)) : 0.f;
   int rc = rr_init_launch(w.rr.Z, d, p, Q0, k0, ldq0, 0x5eed5eedull, st);
   if (rc) return rc;
   float best = 3.4e38f;
@@ -169,7 +171,7 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
     if ((rc = apply_op(op, w, d, p, st))) return rc;
     if (it > 0 && ++since_rr < rr_every && it + 1 < max_sweeps) {
       // power step on the live Ritz columns of the last RR (Q_j <- Y_j / ||Y w_j||)
-      if ((rc = rr_power_launch(w.rr, d, p, st))) return rc;
+      if ((rc = rr_power_launch(w.rr, d, p, tau, st))) return rc;
       continue;
     }
     since_rr = 0;

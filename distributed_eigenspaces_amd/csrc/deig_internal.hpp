@@ -73,7 +73,7 @@ int skinny_launch(bool trans_a, const float* A, int64_t lda, const float* B, int
                   float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha,
                   float beta, float* slab, size_t slab_bytes, hipStream_t stream);
 
-// Split-bf16 symmetric sweep (sweep.hip): Y = alpha * S Q, S symmetric d x d
+// bf16x6 symmetric sweep (sweep.hip): Y = alpha * S Q, S symmetric d x d
 // row-major, Q d x p (ldq), Y d x p (ldy), p % 16 == 0, p <= 128.
 size_t sweep_workspace_bytes(int64_t d, int p);
 int sweep_launch(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
@@ -96,7 +96,7 @@ int rr_init_launch(float* Z, int64_t d, int p, const float* Q0, int k0, int64_t 
                    uint64_t seed, hipStream_t stream);
 int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream);
 int rr_update_blocks(int64_t d);
-int rr_power_launch(const RRBuffers& b, int64_t d, int p, hipStream_t stream);
+int rr_power_launch(const RRBuffers& b, int64_t d, int p, float tau, hipStream_t stream);
 int rr_update_launch(const RRBuffers& b, int64_t d, int p, int k, float* V, int64_t ldv,
                      float* evals, hipStream_t stream);
 

@@ -435,21 +435,23 @@ __global__ __launch_bounds__(256) void rr_finish_kernel(const float* __restrict_
 
 // Power step between two Rayleigh-Ritz sweeps: Q_j <- Y_j * cs_j for the live
 // Ritz columns of the last RR (cs_j = 1 / ||Y w_j||, so the columns stay ~unit
-// norm) whose Ritz value is within 10x of the largest.  Dead columns (cs_j == 0:
-// null directions of a rank-deficient operator) keep Q_j, as rr_update treats
-// them, and so do weak columns: an extra power step multiplies their
-// contamination by the dominant directions by |lambda_0 / lambda_j| before the
-// next RR re-orthogonalises, which for a wide spectrum (the projector average:
-// 1 vs << 1) makes the basis numerically dependent.
+// norm) whose Ritz value satisfies |lambda_j| >= tau |lambda_0|.  Dead columns
+// (cs_j == 0: null directions of a rank-deficient operator) keep Q_j, as
+// rr_update treats them, and so do weak columns: every extra power step
+// multiplies a column's contamination by the dominant directions by up to
+// |lambda_0 / lambda_j| before the next RR re-orthogonalises, so the driver
+// picks tau = 0.1^(1 / steps between RRs) and the growth stays <= 10x (a wide
+// spectrum - the projector average: 1 vs << 1 - would otherwise make the
+// basis numerically dependent).
 __global__ __launch_bounds__(256) void rr_power_kernel(float* __restrict__ Z, int64_t d, int p,
                                                        const float* __restrict__ cs,
-                                                       const float* __restrict__ lam) {
+                                                       const float* __restrict__ lam, float tau) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= d * p) return;
   const int64_t r = idx / p;
   const int j = (int)(idx - r * p);
   const float c = cs[j];
-  if (c > 0.f && fabsf(lam[j]) >= 0.1f * fabsf(lam[0])) Z[r * 2 * p + j] = Z[r * 2 * p + p + j] * c;
+  if (c > 0.f && fabsf(lam[j]) >= tau * fabsf(lam[0])) Z[r * 2 * p + j] = Z[r * 2 * p + p + j] * c;
 }
 
 size_t rr_small_shm(int p) {
@@ -483,9 +485,9 @@ int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream) {
   return DEIG_OK;
 }
 
-int rr_power_launch(const RRBuffers& b, int64_t d, int p, hipStream_t stream) {
+int rr_power_launch(const RRBuffers& b, int64_t d, int p, float tau, hipStream_t stream) {
   hipLaunchKernelGGL(rr_power_kernel, dim3((unsigned)cdiv(d * p, 256)), dim3(256), 0, stream, b.Z,
-                     d, p, b.cs, b.lam);
+                     d, p, b.cs, b.lam, tau);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }
