@@ -15,6 +15,9 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdeig.so")
 SOURCES = ["capi.hip", "syrk.hip", "syrk_split.hip", "skinny.hip", "rr.hip", "oja.hip", "project.hip",
            "sweep.hip"]
+# Per-source extra flags.  sweep.hip: keep the split's scalar f32 subtractions
+# unpacked (v_pk_add_f32 beside MFMAs costs issue cycles, MI355X_MICROARCH.md).
+EXTRA_FLAGS = {"sweep.hip": ["-fno-slp-vectorize"]}
 HEADERS = ["deig_internal.hpp", os.path.join("..", "..", "include", "deig.h")]
 ARCH = os.environ.get("DEIG_OFFLOAD_ARCH", "gfx950")
 
@@ -46,7 +49,7 @@ def build_library(force: bool = False, verbose: bool = True) -> str:
         obj = os.path.join(tmpdir, src.replace(".hip", ".o"))
         objs.append(obj)
         cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-               "-Wno-unused-function", "-Wno-inline-asm", "-c", os.path.join(CSRC, src), "-o", obj]
+               "-Wno-unused-function", "-Wno-inline-asm"] + EXTRA_FLAGS.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
     for cmd, p in procs:
         out, _ = p.communicate()

@@ -32,7 +32,16 @@ int fail(int code, const char* fmt, ...);
   } while (0)
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
-inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+__host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Bijective XCD-aware relabel of a 1-D grid of G blocks: blocks b, b+8, ... (one
+// XCD under round-robin dispatch) get consecutive logical ids, so neighbouring
+// logical work items share that XCD's L2.
+__device__ __forceinline__ int xcd_logical(int b, int G) {
+  const int x = b & 7, qq = G >> 3, rr = G & 7;
+  const int base = (x < rr) ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq;
+  return base + (b >> 3);
+}
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // Number of CUs of the current device (cached per device id).

@@ -64,14 +64,6 @@ __device__ __forceinline__ void tile_coords(int t, int& ti, int& tj) {
   tj = t - r * (r + 1) / 2;
 }
 
-// Bijective XCD-aware relabel: blocks b, b+8, ... (one XCD under round-robin
-// dispatch) get consecutive logical ids, hence consecutive tiles of one tile-row.
-__device__ __forceinline__ int xcd_logical(int b, int G) {
-  const int x = b & 7, qq = G >> 3, rr = G & 7;
-  const int base = (x < rr) ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq;
-  return base + (b >> 3);
-}
-
 // First block whose remainder range contains work position pos.
 __device__ __forceinline__ int64_t block_of(int64_t pos, int64_t Wr, int G) {
   return ((pos + 1) * (int64_t)G + Wr - 1) / Wr - 1;

@@ -69,12 +69,6 @@ struct SSched {
   int prio;      // 1: waves 4-7 run at s_setprio 1 (the arbitration losers otherwise)
 };
 
-__device__ __forceinline__ int xcd_logical(int b, int G) {
-  const int x = b & 7, qq = G >> 3, rr = G & 7;
-  const int base = (x < rr) ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq;
-  return base + (b >> 3);
-}
-
 __device__ __forceinline__ int64_t block_of(int64_t pos, int64_t Wr, int G) {
   return ((pos + 1) * (int64_t)G + Wr - 1) / Wr - 1;
 }
