@@ -28,8 +28,11 @@
 //   syrks_reduce   split-K remainder tiles, summed in block order (deterministic);
 //   diag_corr      S[i][i] += alpha * sum lo_i^2.
 // Tile order: 8 x 4 super-tiles of the lower triangle, so the ~32 tiles an XCD
-// runs concurrently share few panels in its L2.  Work decomposition (phases +
-// K-split remainder, no atomics) is the one of syrk.hip.
+// runs concurrently share few panels in its L2.  Work decomposition (no
+// atomics): q = T / G full phases of one tile per block; the R = T mod G
+// remainder tiles are cut into nseg equal K segments run K-synchronously
+// (segment-major item order) and summed in segment order by syrks_reduce.
+#include <cmath>
 #include <cstdlib>
 
 #include "deig_internal.hpp"
@@ -56,12 +59,12 @@ constexpr size_t DEFAULT_CHUNK_BYTES = size_t(64) << 30;
 struct SSched {
   const unsigned char* XP;  // bf16 image of this chunk
   float* S;
-  float* part;   // 2 remainder slabs per block
+  float* part;   // one slab per remainder item
   float* accs;   // 1 flush slab per block
   const int* order;  // tile order: ti | tj << 16
   int64_t lds, dp;
   int64_t NK;  // K-tiles in the chunk
-  int64_t Wr;  // remainder work items (R * NK)
+  int nseg;    // K segments per remainder tile (items = R * nseg)
   int d, nt, T, G, q, R;
   float alpha;
   int beta;
@@ -69,9 +72,6 @@ struct SSched {
   int prio;      // 1: waves 4-7 run at s_setprio 1 (the arbitration losers otherwise)
 };
 
-__device__ __forceinline__ int64_t block_of(int64_t pos, int64_t Wr, int G) {
-  return ((pos + 1) * (int64_t)G + Wr - 1) / Wr - 1;
-}
 
 __device__ __forceinline__ i32x4 make_rsrc(const void* base, uint32_t nrec) {
   const uint64_t a = reinterpret_cast<uint64_t>(base);
@@ -346,13 +346,13 @@ __device__ __forceinline__ void store4(const SSched& s, int ib, int j, bool diag
 }
 
 template <int MF, int KT, int NST>
-__device__ void segment(const SSched& s, unsigned char* lds, int tile, int64_t k0, int64_t k1,
+__device__ __forceinline__ void segment(const SSched& s, unsigned char* lds, int tile, int64_t k0, int64_t k1,
                         int slot, bool partial) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wi = wave >> 2, wj = wave & 3;
   const int lane16 = lane * 16;
-  const int tt = s.order[tile];
+  const int tt = __builtin_amdgcn_readfirstlane(s.order[tile]);
   const int ti = tt & 0xffff, tj = tt >> 16;
   const int i0 = ti * BT, j0 = tj * BT;
   const bool diag = (ti == tj);
@@ -419,34 +419,30 @@ __global__ __launch_bounds__(NTHR) void syrks_kernel(SSched s) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[NST * Geo<KT>::BUF_B];
   const int b = blockIdx.x;
   const int L = xcd_logical(b, s.G);
-  int64_t pos = 0, end = 0;
-  if (s.R > 0) {
-    pos = (int64_t)b * s.Wr / s.G;
-    end = (int64_t)(b + 1) * s.Wr / s.G;
-  }
-  int m = 0, seg = 0;
-  for (;;) {
+  // Full phases (w < q): every block walks all K of one tile, in lock-step with
+  // the rest.  Remainder: R tiles x nseg equal K segments, item i = seg * R + r,
+  // taken by logical block i mod G in round i / G.  Segment-major numbering
+  // keeps the items that run together (and, by the XCD-aware relabel, the ~G/8
+  // on one XCD) on the same K rows of neighbouring tiles, so their panels are
+  // shared in L2 rather than each item streaming its own K range from HBM.
+  // One call site of segment(): its unrolled body is inlined once.
+  const int items = s.R * s.nseg;
+  const int nwork = s.q + (L < items ? (items - 1 - L) / s.G + 1 : 0);
+  for (int w = 0; w < nwork; ++w) {
     int tile, slot = 0;
-    int64_t k0, k1;
-    bool partial;
-    if (m < s.q) {
-      tile = m * s.G + L;
-      k0 = 0;
-      k1 = s.NK;
-      partial = false;
-      ++m;
-    } else if (pos < end) {
-      const int64_t r = pos / s.NK;
-      k0 = pos - r * s.NK;
-      k1 = k0 + (end - pos);
-      if (k1 > s.NK) k1 = s.NK;
-      tile = s.q * s.G + (int)r;
-      slot = 2 * b + seg;
-      partial = true;
-      pos += k1 - k0;
-      ++seg;
+    int64_t k0 = 0, k1 = s.NK;
+    const bool partial = w >= s.q;
+    if (!partial) {
+      tile = w * s.G + L;
     } else {
-      break;
+      const int i = L + (w - s.q) * s.G;
+      const int sg = i / s.R, r = i - sg * s.R;
+      tile = s.q * s.G + r;
+      slot = i;
+      // (64-bit divisions run on the VALU: pin the bounds to SGPRs, the DMA
+      // descriptors built from them must be wave-uniform)
+      k0 = __builtin_amdgcn_readfirstlane((int)(s.NK * sg / s.nseg));
+      k1 = __builtin_amdgcn_readfirstlane((int)(s.NK * (sg + 1) / s.nseg));
     }
     segment<MF, KT, NST>(s, lds, tile, k0, k1, slot, partial);
   }
@@ -462,15 +458,9 @@ __global__ __launch_bounds__(256) void syrks_reduce_kernel(SSched s) {
   const int tt = s.order[s.q * s.G + r];
   const int ti = tt & 0xffff, tj = tt >> 16;
   const bool diag = (ti == tj);
-  const int64_t pos0 = (int64_t)r * s.NK, pos1 = pos0 + s.NK;
-  const int64_t bf = block_of(pos0, s.Wr, s.G), bl = block_of(pos1 - 1, s.Wr, s.G);
   f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t b = bf; b <= bl; ++b) {
-    const int64_t sb = b * s.Wr / s.G, eb = (b + 1) * s.Wr / s.G;
-    if (eb <= sb || eb <= pos0 || sb >= pos1) continue;
-    const int64_t slot = 2 * b + (sb < pos0 ? 1 : 0);
-    sum += *reinterpret_cast<const f32x4*>(s.part + slot * SLAB + (int64_t)f * 4);
-  }
+  for (int sg = 0; sg < s.nseg; ++sg)  // fixed order: deterministic
+    sum += *reinterpret_cast<const f32x4*>(s.part + (int64_t)(sg * s.R + r) * SLAB + (int64_t)f * 4);
   const float a[4] = {sum[0], sum[1], sum[2], sum[3]};
   store4(s, ti * BT + 128 * wi + Acc<MF>::qrow(q, lane), tj * BT + 64 * wj + Acc<MF>::qcol(q, lane),
          diag, a);
@@ -555,12 +545,27 @@ __global__ void tile_order_kernel(int nt, int* order) {
   }
 }
 
+// K segments per remainder tile: the smallest nseg (<= 64) whose critical path
+// ceil(R nseg / G) / nseg (in full-tile passes) is within 2 % of the best.
+int remainder_segments(int64_t R, int G) {
+  if (R <= 0) return 0;
+  if (const char* v = getenv("DEIG_SYRK_SEGS")) {
+    const int e = atoi(v);
+    if (e >= 1 && e <= 256) return e;
+  }
+  double best = 1e30;
+  for (int k = 1; k <= 64; ++k) best = fmin(best, (double)cdiv(R * k, G) / k);
+  for (int k = 1; k <= 64; ++k)
+    if ((double)cdiv(R * k, G) / k <= best * 1.02) return k;
+  return 1;
+}
+
 struct Layout {
-  int64_t dp, nt, T, G, q, R, yb_max, chunk_rows;
+  int64_t dp, nt, T, G, q, R, nseg, yb_max, chunk_rows;
   size_t off_order, off_accs, off_part, off_corr, off_xp, total;
 };
 
-// Workspace: [order][G flush slabs][2G remainder slabs][corr YB x dp][XP chunk].
+// Workspace: [order][G flush slabs][R * nseg remainder slabs][corr YB x dp][XP chunk].
 Layout make_layout(int64_t n, int64_t d, int G, int64_t chunk_rows) {
   Layout L;
   L.dp = cdiv(d, BT) * BT;
@@ -569,6 +574,7 @@ Layout make_layout(int64_t n, int64_t d, int G, int64_t chunk_rows) {
   L.G = G;
   L.q = L.T / G;
   L.R = L.T % G;
+  L.nseg = remainder_segments(L.R, G);
   L.yb_max = SPLIT_YB;
   L.chunk_rows = chunk_rows;
   size_t off = 0;
@@ -577,7 +583,7 @@ Layout make_layout(int64_t n, int64_t d, int G, int64_t chunk_rows) {
   L.off_accs = off;
   off += sizeof(float) * (size_t)G * SLAB;
   L.off_part = off;
-  if (L.R > 0) off += sizeof(float) * (size_t)2 * G * SLAB;
+  off += sizeof(float) * (size_t)(L.R * L.nseg) * SLAB;
   L.off_corr = off;
   off = align_up(off + sizeof(float) * (size_t)L.yb_max * L.dp, 256);
   L.off_xp = off;
@@ -669,7 +675,7 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
                        stream, X + r0 * ldx, rows, ldx, (int)d, L.dp, noct, xp, corr);
     DEIG_HIP_CHECK(hipGetLastError());
     s.NK = nk;
-    s.Wr = (int64_t)s.R * nk;
+    s.nseg = (int)L.nseg;
     s.beta = c > 0 ? 1 : 0;
     s.flush_kt = (int)(flush_rows / (16 * kt_steps));
     const bool mf16 = variant >= 100;
