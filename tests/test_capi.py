@@ -29,8 +29,11 @@ def test_workspace_queries():
     slabs = 3 * 256 * 256 * 256 * 4
     assert L.deig_syrk_workspace_ex(n, d, _lib.DEIG_SYRK_FP32) == slabs
     # split3 adds the bf16 hi/lo image of the shard (4 B per sample value, one chunk)
+    # split3: one flush slab per CU + the 16 remainder tiles cut into 16 K-synchronous
+    # segments (16 x 16 slabs), see syrk_split.hip remainder_segments()
     ws = L.deig_syrk_workspace_ex(n, d, _lib.DEIG_SYRK_SPLIT3)
-    assert n * d * 4 + slabs <= ws <= n * d * 4 + slabs + (16 << 20)
+    split_slabs = (256 + 16 * 16) * 256 * 256 * 4
+    assert n * d * 4 + split_slabs <= ws <= n * d * 4 + split_slabs + (16 << 20)
     assert L.deig_syrk_workspace(n, d) == ws  # default = auto = split3 at n >= 1024
     assert L.deig_syrk_workspace(1000, 256) == L.deig_syrk_workspace_ex(1000, 256,
                                                                         _lib.DEIG_SYRK_FP32)
