@@ -27,6 +27,7 @@ SYRK_ALGOS = {"auto": DEIG_SYRK_AUTO, "split3": DEIG_SYRK_SPLIT3, "fp32": DEIG_S
 DEIG_SWEEP_AUTO = 0
 DEIG_SWEEP_BF16X6 = 1
 DEIG_SWEEP_FP32 = 2
+DEIG_SWEEP_PREPARED = 0x100
 SWEEP_ALGOS = {"auto": DEIG_SWEEP_AUTO, "bf16x6": DEIG_SWEEP_BF16X6, "fp32": DEIG_SWEEP_FP32}
 
 _c_i64 = ctypes.c_int64

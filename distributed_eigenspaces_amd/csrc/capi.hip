@@ -122,7 +122,7 @@ int apply_op(const Operator& op, const SolverWs& w, int64_t d, int p, hipStream_
   const int64_t ld = 2 * p;
   if (!op.implicit) {
     if (w.sweep_ws)
-      return sweep_launch(op.S, d, op.lds, Q, p, ld, Y, ld, 1.f, w.sweep_ws, w.sweep_bytes, st);
+      return sweep_apply(op.S, d, op.lds, Q, p, ld, Y, ld, 1.f, w.sweep_ws, w.sweep_bytes, st);
     return skinny_launch(true, op.S, op.lds, Q, ld, Y, ld, d, p, d, 1.f, 0.f, w.slab,
                          w.slab_bytes, st);
   }
@@ -166,6 +166,9 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
   const float tau = rr_every > 1 ? powf(0.1f, 1.0f / (float)(rr_every - 1)) : 0.f;
   int rc = rr_init_launch(w.rr.Z, d, p, Q0, k0, ldq0, 0x5eed5eedull, st);
   if (rc) return rc;
+  if (!op.implicit && w.sweep_ws &&
+      (rc = sweep_prepare(op.S, d, op.lds, p, w.sweep_ws, w.sweep_bytes, st)))
+    return rc;
   float best = 3.4e38f;
   int since_best = 0;
   int since_rr = 0;
@@ -328,9 +331,15 @@ int deig_sym_apply_f32(const float* S, int64_t d, int64_t lds, const float* Q, i
   if (algo == DEIG_SWEEP_FP32)
     return skinny_launch(true, S, lds, Q, ldq, Y, ldy, d, p, d, alpha, 0.f,
                          static_cast<float*>(ws), ws_bytes, (hipStream_t)stream);
+  const bool prepared = (algo & DEIG_SWEEP_PREPARED) != 0;
+  algo &= ~DEIG_SWEEP_PREPARED;
   if (algo != DEIG_SWEEP_AUTO && algo != DEIG_SWEEP_BF16X6)
     return fail(DEIG_EINVAL, "sym_apply: unknown algorithm %d", algo);
-  return sweep_launch(S, d, lds, Q, p, ldq, Y, ldy, alpha, ws, ws_bytes, (hipStream_t)stream);
+  if (!prepared) {
+    const int rc = sweep_prepare(S, d, lds, p, ws, ws_bytes, (hipStream_t)stream);
+    if (rc) return rc;
+  }
+  return sweep_apply(S, d, lds, Q, p, ldq, Y, ldy, alpha, ws, ws_bytes, (hipStream_t)stream);
 }
 
 size_t deig_oja_workspace(int64_t b, int64_t d, int k) { return oja_workspace_bytes(b, d, k); }

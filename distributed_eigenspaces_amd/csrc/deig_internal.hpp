@@ -87,6 +87,13 @@ int skinny_launch(bool trans_a, const float* A, int64_t lda, const float* B, int
 size_t sweep_workspace_bytes(int64_t d, int p);
 int sweep_launch(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
                  float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st);
+// The same in two parts: sweep_prepare builds the S image in the workspace (once
+// per S), sweep_apply runs one product from it (S is still passed: the v1 kernel
+// reads it in place).
+int sweep_prepare(const float* S, int64_t d, int64_t lds, int p, void* ws, size_t ws_bytes,
+                  hipStream_t st);
+int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
+                float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st);
 
 // Rayleigh-Ritz pieces (rr.hip).
 struct RRBuffers {

@@ -260,6 +260,356 @@ __global__ __launch_bounds__(SW_THR) void sweep_kernel(const float* __restrict__
       }
 }
 
+// ---------------------------------------------------------------- sweep v2
+// S image: S re-laid once per solve (sweep_prepare_kernel) in MFMA A-operand
+// order so that every wave streams one contiguous run of HBM:
+//   [64-row block rb][k-group g (32 k)][m-block mb (4)][half h (2)][lane][16 B],
+// lane l of (rb, g, mb, h) holding S[64 rb + 16 mb + l%16][32 g + 8 (l/16) + 4 h .. +3].
+// One (rb, g) chunk is 8 KiB; rows are padded to a multiple of 256 and columns
+// to a multiple of 32 with zeros (no masking, no range checks in the sweep).
+// Row-major S read 16 rows x 128 B per wave-instruction streamed at ~4 TB/s
+// (knock-out: S loads + split alone 65 us at d = 8192); the image is read in
+// 1-KiB contiguous wave-instructions.
+constexpr int SI_RB = 64;    // rows per image row block (one wave)
+constexpr int SI_BR = 256;   // rows per sweep2 block (4 waves)
+
+__host__ __device__ inline int64_t si_rows(int64_t d) { return cdiv(d, SI_BR) * SI_BR; }
+__host__ __device__ inline int64_t si_groups(int64_t d) { return cdiv(d, 32); }
+size_t si_bytes(int64_t d) { return (size_t)si_rows(d) * si_groups(d) * 32 * 4; }
+
+// One thread per (rb, g, mb, lane): reads 32 contiguous bytes of one row, writes
+// the two 16-B halves (h = 0, 1) 1 KiB apart (d = 8192: 88 us = 6.1 TB/s of
+// read + write; an LDS-transposed variant with whole-row reads took 131 us).
+__global__ __launch_bounds__(256) void sweep_prepare_kernel(const float* __restrict__ S,
+                                                            int64_t lds, int64_t d, int64_t ng,
+                                                            int64_t nunits,
+                                                            f32x4* __restrict__ SI) {
+  const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (u >= nunits) return;
+  const int lane = (int)(u & 63);
+  const int mb = (int)((u >> 6) & 3);
+  const int64_t t = u >> 8;  // rb * ng + g
+  const int64_t rb = t / ng, g = t - rb * ng;
+  const int64_t row = SI_RB * rb + 16 * mb + (lane & 15);
+  const int64_t k = 32 * g + 8 * (lane >> 4);
+  f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = {0.f, 0.f, 0.f, 0.f};
+  if (row < d) {
+    const float* src = S + row * lds + k;
+    if (k + 8 <= d) {
+      v0 = *reinterpret_cast<const f32x4*>(src);
+      v1 = *reinterpret_cast<const f32x4*>(src + 4);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (k + e < d) v0[e] = src[e];
+        if (k + 4 + e < d) v1[e] = src[4 + e];
+      }
+    }
+  }
+  f32x4* dst = SI + ((t * 4 + mb) * 2) * 64 + lane;
+  dst[0] = v0;
+  dst[64] = v1;
+}
+
+// Sweep kernel v2: independent waves, no LDS, no barriers.
+//
+// Each wave owns 64 rows (MB = 4 m-blocks) of the S image and one split-K
+// slice of k-groups.  Per k-group it loads its 8 KiB of S (8 x 1 KiB, one
+// contiguous run from HBM) and the group's Q image fragments (NB x 3 x 1 KiB
+// from L2: the XCD-aware slice order keeps an XCD on one slice of the image),
+// splits S into h/m/l in registers and issues MB * NB * 6 MFMAs.  Q reuse is
+// MB m-blocks per fragment, so the image is read from L2 p*6/256 times as many
+// bytes as S from HBM (1.9x at p = 80), but there is no block-wide lock-step:
+// the four waves of a CU (one per SIMD, up to 512 registers each) stream
+// independently, each with a D-deep register ring of S and Q fragments.
+// PROBE (diagnostic builds only, DEIG_SWEEP_PROBE): bit 0 drops the MFMAs, bit 1
+// the S loads, bit 2 the Q loads (results are then garbage).
+template <int NB, int PROBE = 0>
+__global__ __launch_bounds__(256, 1) void sweep2_kernel(const f32x4* __restrict__ SI, int64_t d,
+                                                        const u32x4* __restrict__ QS,
+                                                        int64_t ngrp, float* __restrict__ Y,
+                                                        int64_t ldy, float alpha,
+                                                        float* __restrict__ part) {
+  constexpr int MB = 4;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, gq = lane >> 4;
+  const int bx = (int)cdiv(d, SI_BR);
+  const int ks = (int)(gridDim.x / bx);
+  const int lid = xcd_logical(blockIdx.x, gridDim.x);
+  const int sl = lid / bx;
+  const int64_t rb = (int64_t)(lid - sl * bx) * (SI_BR / SI_RB) + wave;
+  const int64_t row0 = rb * SI_RB;
+  const int64_t c0 = ngrp * sl / ks, c1 = ngrp * (sl + 1) / ks;
+
+  f32x4 acc[MB][NB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[mb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Register rings: S rows of 3 groups (the split runs one group ahead of the
+  // MFMAs, so S is needed two bodies after its load is issued), Q fragments of
+  // 2 groups, S pieces of 2 groups (the MFMAs of group g read set g & 1 while
+  // the split of group g + 1 fills the other, interleaved with them).
+  const f32x4* sw = SI + rb * ngrp * (MB * 2 * 64) + lane;
+  f32x4 sr[3][MB][2];
+  u32x4 qf[2][NB][3];
+  u32x4 pc[2][3][MB];
+  auto clampg = [&](int64_t g) { return g < c1 ? g : c1 - 1; };
+  auto load_s = [&](int b, int64_t g) {
+    const f32x4* sg = sw + clampg(g) * (MB * 2 * 64);
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if constexpr (PROBE & 2)
+          sr[b][mb][h] = f32x4{(float)g, (float)mb, (float)h, (float)lane};
+        else
+          sr[b][mb][h] = sg[(mb * 2 + h) * 64];
+      }
+  };
+  auto load_q = [&](int b, int64_t g) {
+    const u32x4* qg = QS + clampg(g) * (NB * 3 * 64) + lane;
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int p3 = 0; p3 < 3; ++p3) {
+        if constexpr (PROBE & 4)
+          qf[b][j][p3] = u32x4{(unsigned)g, (unsigned)j, (unsigned)p3, (unsigned)lane};
+        else
+          qf[b][j][p3] = qg[(j * 3 + p3) * 64];
+      }
+  };
+  auto split_into = [&](int ps, int b) {
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+      split8(sr[b][mb][0], sr[b][mb][1], pc[ps][0][mb], pc[ps][1][mb], pc[ps][2][mb]);
+  };
+  // Body of group g: S slot of g + 1 is SB1 = (g + 1) % 3, Q slot / piece set
+  // QB = g & 1.  The tail loads and splits clamped copies of the last group.
+  auto body = [&](auto SBc, auto QBc, int64_t g) {
+    constexpr int SB1 = decltype(SBc)::value, QB = decltype(QBc)::value;
+    const u32x4(&ah)[MB] = pc[QB][0];
+    const u32x4(&am)[MB] = pc[QB][1];
+    const u32x4(&al)[MB] = pc[QB][2];
+    split_into(QB ^ 1, SB1);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const u32x4 bh = qf[QB][j][0], bm = qf[QB][j][1], bl = qf[QB][j][2];
+      if constexpr (PROBE & 1) {
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+          acc[mb][j][0] += __uint_as_float((ah[mb][0] ^ am[mb][1] ^ al[mb][2] ^ bh[0] ^ bm[1] ^ bl[2]) & 0x3fffffffu);
+        continue;
+      }
+      // small terms first; MB independent accumulators between dependent MFMAs
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(am[mb], bm, acc[mb][j]);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bl, acc[mb][j]);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(al[mb], bh, acc[mb][j]);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bm, acc[mb][j]);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(am[mb], bh, acc[mb][j]);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bh, acc[mb][j]);
+    }
+    load_q(QB, g + 2);   // the Q slot just consumed
+    load_s(SB1, g + 4);  // the S slot just split
+    // Keep the refills here: at this register pressure the scheduler otherwise
+    // sinks the loads next to their use (a vmcnt(0) per group).
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+
+  if (c0 < c1) {
+    load_s(0, c0);
+    load_q(0, c0);
+    load_s(1, c0 + 1);
+    load_q(1, c0 + 1);
+    load_s(2, c0 + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    split_into(0, 0);  // S(c0) -> piece set 0; slot 0 then takes S(c0 + 3)
+    load_s(0, c0 + 3);
+    __builtin_amdgcn_sched_barrier(0);
+    // Six bodies per trip: S slot of g + 1 = (g + 1) % 3, Q slot = g & 1.
+    int64_t g = c0;
+    for (; g + 6 <= c1; g += 6) {
+      body(I1{}, I0{}, g);
+      body(I2{}, I1{}, g + 1);
+      body(I0{}, I0{}, g + 2);
+      body(I1{}, I1{}, g + 3);
+      body(I2{}, I0{}, g + 4);
+      body(I0{}, I1{}, g + 5);
+    }
+    if (g < c1) body(I1{}, I0{}, g);
+    if (g + 1 < c1) body(I2{}, I1{}, g + 1);
+    if (g + 2 < c1) body(I0{}, I0{}, g + 2);
+    if (g + 3 < c1) body(I1{}, I1{}, g + 3);
+    if (g + 4 < c1) body(I2{}, I0{}, g + 4);
+  }
+
+  constexpr int P = 16 * NB;
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t row = row0 + 16 * mb + 4 * gq + e;
+        if (row < d) {
+          if (ks == 1)
+            Y[row * ldy + 16 * j + r] = alpha * acc[mb][j][e];
+          else
+            part[((int64_t)sl * d + row) * P + 16 * j + r] = acc[mb][j][e];
+        }
+      }
+}
+
+// Sweep kernel v3: v2's S image stream with the Q image shared through LDS.
+//
+// v2 loads every Q fragment into every wave (1.9x the S bytes through the CU's
+// load path at p = 80; knock-outs: S + Q loads alone 62 us vs S alone 47 us).
+// Here the four waves of a block DMA each k-group's Q image (3 NB KiB, 1-KiB
+// pieces spread over the waves) into a (D + 1)-slot LDS ring with
+// buffer_load ... lds, issued D groups ahead together with the S registers, and
+// read the fragments back with conflict-free ds_read_b128: Q traffic drops to
+// p*6/1024 of the S bytes.  One raw s_barrier per group publishes the slot
+// (the DMA of group g is older than the S loads of group g, so the wait for
+// those covers it); the slot refilled at group g was last read at g - 1.
+__device__ __forceinline__ void sw_dma16(const __amdgpu_buffer_rsrc_t rsrc, int voff,
+                                         const void* lds_dst) {
+  const unsigned m0v = (unsigned)(uintptr_t)(lds_void*)lds_dst;
+  asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               :
+               : "v"(voff), "s"(rsrc), "s"(m0v)
+               : "memory", "m0");
+}
+
+template <int NB, int D>
+__global__ __launch_bounds__(256, 1) void sweep3_kernel(const f32x4* __restrict__ SI, int64_t d,
+                                                        const u32x4* __restrict__ QS,
+                                                        int64_t ngrp, float* __restrict__ Y,
+                                                        int64_t ldy, float alpha,
+                                                        float* __restrict__ part) {
+  constexpr int MB = 4;
+  constexpr int U = 3 * NB;          // 1-KiB Q pieces per k-group
+  constexpr int ND = (U + 3) / 4;    // DMAs per wave per group (tail pieces repeated)
+  constexpr int SLOT = U * 1024;     // bytes per ring slot
+  constexpr int NS = D + 1;          // ring slots
+  static_assert(NS * SLOT <= 160 * 1024, "Q ring exceeds LDS");
+  __shared__ __attribute__((aligned(16))) unsigned char qlds[NS * SLOT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, gq = lane >> 4;
+  const int bx = (int)cdiv(d, SI_BR);
+  const int ks = (int)(gridDim.x / bx);
+  const int lid = xcd_logical(blockIdx.x, gridDim.x);
+  const int sl = lid / bx;
+  const int64_t rb = (int64_t)(lid - sl * bx) * (SI_BR / SI_RB) + wave;
+  const int64_t row0 = rb * SI_RB;
+  const int64_t c0 = ngrp * sl / ks, c1 = ngrp * (sl + 1) / ks;
+
+  f32x4 acc[MB][NB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[mb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<u32x4*>(QS), 0, (int)(ngrp * U * 1024), 0x00020000);
+  const f32x4* sw = SI + rb * ngrp * (MB * 2 * 64) + lane;
+  f32x4 sr[D][MB][2];
+  auto load = [&](int b, int64_t g) {
+    // Q pieces first: the compiler's wait for this group's S registers then
+    // also covers them.
+    unsigned char* slot = qlds + (int)(g % NS) * SLOT;
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+      const int u = wave + 4 * i < U ? wave + 4 * i : U - 1;
+      sw_dma16(qrs, (int)((g * U + u) * 1024) + lane * 16, slot + u * 1024);
+    }
+    const f32x4* sg = sw + g * (MB * 2 * 64);
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) sr[b][mb][h] = sg[(mb * 2 + h) * 64];
+  };
+  auto body = [&](auto Bc, int64_t g) {
+    constexpr int B = decltype(Bc)::value;
+    // Everything issued before the D - 1 younger groups has landed: this
+    // group's Q pieces (every wave's, after the barrier) and S registers.
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"((D - 1) * (ND + 2 * MB))
+                 : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    u32x4 ah[MB], am[MB], al[MB];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) split8(sr[B][mb][0], sr[B][mb][1], ah[mb], am[mb], al[mb]);
+    const u32x4* qs = reinterpret_cast<const u32x4*>(qlds + (int)(g % NS) * SLOT) + lane;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const u32x4 bh = qs[(j * 3 + 0) * 64], bm = qs[(j * 3 + 1) * 64], bl = qs[(j * 3 + 2) * 64];
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(am[mb], bm, acc[mb][j]);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bl, acc[mb][j]);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(al[mb], bh, acc[mb][j]);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bm, acc[mb][j]);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(am[mb], bh, acc[mb][j]);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bh, acc[mb][j]);
+    }
+    // Refill D groups ahead (clamped: the tail re-loads the last group into its
+    // own slot, which holds the same bytes, so no reader sees a change).
+    const int64_t pf = g + D < c1 ? g + D : c1 - 1;
+    load(B, pf);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  if (c0 < c1) {
+#pragma unroll
+    for (int b = 0; b < D; ++b) load(b, c0 + b < c1 ? c0 + b : c1 - 1);
+    __builtin_amdgcn_sched_barrier(0);
+    int64_t g = c0;
+    for (; g + D <= c1; g += D) {
+      body(std::integral_constant<int, 0>{}, g);
+      body(std::integral_constant<int, 1>{}, g + 1);
+      if constexpr (D > 2) body(std::integral_constant<int, 2>{}, g + 2);
+      if constexpr (D > 3) body(std::integral_constant<int, 3>{}, g + 3);
+    }
+    if (g < c1) body(std::integral_constant<int, 0>{}, g);
+    if (g + 1 < c1) body(std::integral_constant<int, 1>{}, g + 1);
+    if constexpr (D > 3)
+      if (g + 2 < c1) body(std::integral_constant<int, 2>{}, g + 2);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the block's LDS
+
+  constexpr int P = 16 * NB;
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t row = row0 + 16 * mb + 4 * gq + e;
+        if (row < d) {
+          if (ks == 1)
+            Y[row * ldy + 16 * j + r] = alpha * acc[mb][j][e];
+          else
+            part[((int64_t)sl * d + row) * P + 16 * j + r] = acc[mb][j][e];
+        }
+      }
+}
+
 __global__ __launch_bounds__(256) void sweep_reduce_kernel(const float* __restrict__ part, int ks,
                                                            int64_t d, int p, float alpha,
                                                            float* __restrict__ Y, int64_t ldy) {
@@ -294,59 +644,171 @@ int sweep_ks(int64_t d) {
 // Q image: 3 bf16 pieces per value
 size_t qs_bytes(int64_t d, int p) { return (size_t)cdiv(d, SW_KS) * SW_KS * p * 6; }
 
+// Kernel version: 0 = default (v2 for p <= 80, v3 above, where v2's register
+// rings spill), 2 (S image, independent waves with Q in registers), 3 (S image,
+// LDS-shared Q ring) or 1 (row-major S, register-staged Q stage, 8 waves);
+// DEIG_SWEEP_KERNEL selects one, for A/B timing.
+int sweep_version() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DEIG_SWEEP_KERNEL");
+    v = (e && atoi(e) >= 1 && atoi(e) <= 3) ? atoi(e) : 0;
+  }
+  return v;
+}
+
 template <int NB>
-void launch_nb(dim3 grid, hipStream_t st, const float* S, int64_t lds, int64_t d, const u32x4* QS,
-               int64_t nsteps, float* Y, int64_t ldy, float alpha, float* part) {
-  hipLaunchKernelGGL(sweep_kernel<NB>, grid, dim3(SW_THR), 0, st, S, lds, d, QS, nsteps, Y, ldy,
-                     alpha, part);
+void launch_v1(dim3 grid, hipStream_t st, const float* S, int64_t lds, int64_t d, const u32x4* QS,
+               float* Y, int64_t ldy, float alpha, float* part) {
+  hipLaunchKernelGGL(sweep_kernel<NB>, grid, dim3(SW_THR), 0, st, S, lds, d, QS, cdiv(d, SW_KS),
+                     Y, ldy, alpha, part);
+}
+
+template <int NB>
+void launch_v2(dim3 grid, hipStream_t st, const f32x4* SI, int64_t d, const u32x4* QS, float* Y,
+               int64_t ldy, float alpha, float* part) {
+  const int64_t ng = si_groups(d);
+  if constexpr (NB == 5) {
+    static const int probe = getenv("DEIG_SWEEP_PROBE") ? atoi(getenv("DEIG_SWEEP_PROBE")) : 0;
+    switch (probe) {
+#define DEIG_PROBE_CASE(P_)                                                                   \
+  case P_:                                                                                   \
+    hipLaunchKernelGGL((sweep2_kernel<NB, P_>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy, \
+                       alpha, part);                                                         \
+    return;
+      DEIG_PROBE_CASE(1) DEIG_PROBE_CASE(2) DEIG_PROBE_CASE(3) DEIG_PROBE_CASE(4)
+      DEIG_PROBE_CASE(5) DEIG_PROBE_CASE(6) DEIG_PROBE_CASE(7)
+#undef DEIG_PROBE_CASE
+      default: break;
+    }
+  }
+  hipLaunchKernelGGL((sweep2_kernel<NB>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy, alpha,
+                     part);
+}
+
+template <int NB>
+void launch_v3(dim3 grid, hipStream_t st, const f32x4* SI, int64_t d, const u32x4* QS, float* Y,
+               int64_t ldy, float alpha, float* part) {
+  static const int de = getenv("DEIG_SWEEP_DEPTH") ? atoi(getenv("DEIG_SWEEP_DEPTH")) : 3;
+  const int64_t ng = si_groups(d);
+  if (de == 4)
+    hipLaunchKernelGGL((sweep3_kernel<NB, 4>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy,
+                       alpha, part);
+  else if (de == 2)
+    hipLaunchKernelGGL((sweep3_kernel<NB, 2>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy,
+                       alpha, part);
+  else
+    hipLaunchKernelGGL((sweep3_kernel<NB, 3>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy,
+                       alpha, part);
+}
+
+// Workspace: [Q image][split-K slabs][S image (v2)].
+struct SweepWs {
+  u32x4* QS;
+  float* part;
+  f32x4* SI;
+  size_t total;
+};
+SweepWs sweep_carve(void* ws, int64_t d, int p) {
+  SweepWs w;
+  char* base = static_cast<char*>(ws);
+  size_t off = 0;
+  w.QS = reinterpret_cast<u32x4*>(base + off);
+  off = align_up(off + qs_bytes(d, p), 256);
+  w.part = reinterpret_cast<float*>(base + off);
+  const int ks = sweep_ks(d);
+  if (ks > 1) off = align_up(off + (size_t)ks * d * p * sizeof(float), 256);
+  w.SI = reinterpret_cast<f32x4*>(base + off);
+  if (sweep_version() != 1) off += si_bytes(d);
+  w.total = off;
+  return w;
 }
 
 }  // namespace
 
-size_t sweep_workspace_bytes(int64_t d, int p) {
-  const int ks = sweep_ks(d);
-  size_t total = align_up(qs_bytes(d, p), 256);
-  if (ks > 1) total += (size_t)ks * d * p * sizeof(float);
-  return total;
+size_t sweep_workspace_bytes(int64_t d, int p) { return sweep_carve(nullptr, d, p).total; }
+
+int sweep_prepare(const float* S, int64_t d, int64_t lds, int p, void* ws, size_t ws_bytes,
+                  hipStream_t st) {
+  DEIG_REQUIRE(d >= 1 && lds >= d && lds % 4 == 0 && S && aligned16(S),
+               "sweep: S must be 16-byte aligned with lds >= d, lds %% 4 == 0");
+  const SweepWs w = sweep_carve(ws, d, p);
+  if (!ws || ws_bytes < w.total)
+    return fail(DEIG_EWORKSPACE, "sweep: workspace %zu < %zu", ws_bytes, w.total);
+  if (sweep_version() == 1) return DEIG_OK;  // v1 reads S in place
+  const int64_t ng = si_groups(d);
+  const int64_t nunits = si_rows(d) / SI_RB * ng * 4 * 64;
+  hipLaunchKernelGGL(sweep_prepare_kernel, dim3((unsigned)cdiv(nunits, 256)), dim3(256), 0, st, S,
+                     lds, d, ng, nunits, w.SI);
+  DEIG_HIP_CHECK(hipGetLastError());
+  return DEIG_OK;
 }
 
-int sweep_launch(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
-                 float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st) {
+int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
+                float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st) {
   DEIG_REQUIRE(d >= 1 && p >= 16 && p <= 128 && p % 16 == 0,
                "sweep: need d >= 1 and p in {16, 32, ..., 128} (p=%d)", p);
   DEIG_REQUIRE(lds >= d && lds % 4 == 0 && lds <= (1 << 24) && ldq >= p && ldy >= p,
                "sweep: bad leading dims");
   DEIG_REQUIRE(S && Q && Y && aligned16(S), "sweep: S must be 16-byte aligned");
-  const size_t need = sweep_workspace_bytes(d, p);
-  if (!ws || ws_bytes < need)
-    return fail(DEIG_EWORKSPACE, "sweep: workspace %zu < %zu", ws_bytes, need);
+  const SweepWs w = sweep_carve(ws, d, p);
+  if (!ws || ws_bytes < w.total)
+    return fail(DEIG_EWORKSPACE, "sweep: workspace %zu < %zu", ws_bytes, w.total);
   const int nb = p / 16;
-  const int64_t nsteps = cdiv(d, SW_KS);
-  const int64_t ngrp = 2 * nsteps;
-  u32x4* QS = static_cast<u32x4*>(ws);
-  float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + align_up(qs_bytes(d, p), 256));
+  const int64_t ngrp = 2 * cdiv(d, SW_KS);
   hipLaunchKernelGGL(split_q_kernel, dim3((unsigned)cdiv(ngrp * nb * 64, 256)), dim3(256), 0, st,
-                     Q, ldq, d, nb, ngrp, QS);
+                     Q, ldq, d, nb, ngrp, w.QS);
   DEIG_HIP_CHECK(hipGetLastError());
   const int ks = sweep_ks(d);
   const dim3 grid((unsigned)(cdiv(d, SW_ROWS) * ks));
-  switch (nb) {
-    case 1: launch_nb<1>(grid, st, S, lds, d, QS, nsteps, Y, ldy, alpha, part); break;
-    case 2: launch_nb<2>(grid, st, S, lds, d, QS, nsteps, Y, ldy, alpha, part); break;
-    case 3: launch_nb<3>(grid, st, S, lds, d, QS, nsteps, Y, ldy, alpha, part); break;
-    case 4: launch_nb<4>(grid, st, S, lds, d, QS, nsteps, Y, ldy, alpha, part); break;
-    case 5: launch_nb<5>(grid, st, S, lds, d, QS, nsteps, Y, ldy, alpha, part); break;
-    case 6: launch_nb<6>(grid, st, S, lds, d, QS, nsteps, Y, ldy, alpha, part); break;
-    case 7: launch_nb<7>(grid, st, S, lds, d, QS, nsteps, Y, ldy, alpha, part); break;
-    default: launch_nb<8>(grid, st, S, lds, d, QS, nsteps, Y, ldy, alpha, part); break;
+  if (sweep_version() == 1) {
+    switch (nb) {
+      case 1: launch_v1<1>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 2: launch_v1<2>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 3: launch_v1<3>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 4: launch_v1<4>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 5: launch_v1<5>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 6: launch_v1<6>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 7: launch_v1<7>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
+      default: launch_v1<8>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
+    }
+  } else if (sweep_version() == 3 || (sweep_version() == 0 && nb > 5)) {
+    switch (nb) {
+      case 1: launch_v3<1>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 2: launch_v3<2>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 3: launch_v3<3>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 4: launch_v3<4>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 5: launch_v3<5>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 6: launch_v3<6>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 7: launch_v3<7>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
+      default: launch_v3<8>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
+    }
+  } else {
+    switch (nb) {
+      case 1: launch_v2<1>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 2: launch_v2<2>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 3: launch_v2<3>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 4: launch_v2<4>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 5: launch_v2<5>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 6: launch_v2<6>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
+      case 7: launch_v2<7>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
+      default: launch_v2<8>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
+    }
   }
   DEIG_HIP_CHECK(hipGetLastError());
   if (ks > 1) {
     hipLaunchKernelGGL(sweep_reduce_kernel, dim3((unsigned)cdiv(d * p, 256)), dim3(256), 0, st,
-                       part, ks, d, p, alpha, Y, ldy);
+                       w.part, ks, d, p, alpha, Y, ldy);
     DEIG_HIP_CHECK(hipGetLastError());
   }
   return DEIG_OK;
+}
+
+int sweep_launch(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
+                 float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st) {
+  int rc = sweep_prepare(S, d, lds, p, ws, ws_bytes, st);
+  if (rc) return rc;
+  return sweep_apply(S, d, lds, Q, p, ldq, Y, ldy, alpha, ws, ws_bytes, st);
 }
 
 }  // namespace deig

@@ -86,6 +86,11 @@ int deig_default_subspace(int64_t d, int k);
 #define DEIG_SWEEP_AUTO 0
 #define DEIG_SWEEP_BF16X6 1
 #define DEIG_SWEEP_FP32 2
+/* OR-ed into the algorithm of deig_sym_apply_f32 (BF16X6 only): the workspace
+ * already holds the sweep image of this S from an earlier call with the same
+ * S, d, p and workspace, so the re-layout pass is skipped (repeated products
+ * with one S, as the solver does). */
+#define DEIG_SWEEP_PREPARED 0x100
 
 /* One subspace-iteration sweep Y = alpha * S Q  (S symmetric d x d row-major, lds;
  * Q d x p row-major, ldq; Y d x p row-major, ldy; p % 16 == 0, 16 <= p <= 128).

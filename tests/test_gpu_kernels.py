@@ -204,6 +204,26 @@ def test_sym_apply_sweep(d, p, algo, cuda):
     assert err <= tol, f"sym_apply[{algo}] d={d} p={p}: rel err {err:.3e} > {tol:.1e}"
 
 
+@pytest.mark.parametrize("d,p,ld", [(520, 80, 528), (300, 128, 300), (8192, 64, 8192)])
+def test_sym_apply_prepared_image_reuse(d, p, ld, cuda):
+    """The solver's pattern: the S image is built once (first call), later sweeps
+    with new Q reuse it (DEIG_SWEEP_PREPARED); strided S rows (ld > d)."""
+    import distributed_eigenspaces_amd as de
+    rng = np.random.default_rng(d + p)
+    A = rng.standard_normal((d, d)).astype(np.float32)
+    S = ((A + A.T) * 0.5).astype(np.float32)
+    Sp = np.zeros((d, ld), np.float32)
+    Sp[:, :d] = S
+    Sp[:, d:] = np.nan  # padding columns must never be read
+    St = torch.from_numpy(Sp).to(cuda)[:, :d]
+    for it in range(3):
+        Q = rng.standard_normal((d, p)).astype(np.float32)
+        Y = de.sym_apply(St, torch.from_numpy(Q).to(cuda), algo="bf16x6", prepared=it > 0)
+        ref = S.astype(np.float64) @ Q.astype(np.float64)
+        err = np.abs(Y.cpu().numpy() - ref).max() / np.abs(ref).max()
+        assert err <= 2e-6, f"prepared sweep {it}: rel err {err:.3e}"
+
+
 def test_sym_apply_rejects_bad_p(cuda):
     import distributed_eigenspaces_amd as de
     S = torch.eye(64, device=cuda)
