@@ -223,6 +223,23 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
     float amax = 0.f;
     for (int i = 0; i < RT / 64; ++i) amax = fmaxf(amax, red[i]);
     const float abs_thr = 1e-9f * amax;
+    // Convergence pre-check (one pass, one barrier): if no pair passes the
+    // rotation test now, the first step rotates nothing, the matrix stays as it
+    // is and so does every later step - the sweep would be a no-op.  Saves the
+    // all-identity sweep that used to end every solve (p - 1 steps, 2 barriers each).
+    {
+      int need = 0;
+      for (int idx = tid; idx < p * p && !need; idx += RT) {
+        const int a = idx / p, b = idx - a * p;
+        if (b < a) {
+          const float apq = X1[a * p + b];
+          need = fabsf(apq) > abs_thr &&
+                 fabsf(apq) > 2e-7f * sqrtf(fabsf(X1[a * p + a] * X1[b * p + b]));
+        }
+      }
+      need = __syncthreads_or(need);
+      if (!need) break;
+    }
     for (int st = 0; st < p - 1; ++st) {
       const int ci = 1 + (st & 1);
       if (tid < half) {
