@@ -29,48 +29,74 @@ __global__ __launch_bounds__(256) void rowpad_to_col(const float* __restrict__ V
 }
 
 // G (kp x kp, leading k x k used) = L L^T;  Rinv = L^-T (upper), zero-padded to kp.
-__global__ __launch_bounds__(256) void chol_rinv_kernel(const float* __restrict__ G, int k, int kp,
-                                                        float* __restrict__ Rinv) {
-  __shared__ float L[64 * 64];
-  __shared__ float Li[64 * 64];
-  const int tid = threadIdx.x;
-  for (int idx = tid; idx < k * k; idx += 256) {
-    const int a = idx / k, b = idx - a * k;
-    L[idx] = G[a * kp + b];
-    Li[idx] = 0.f;
-  }
-  __syncthreads();
-  for (int j = 0; j < k; ++j) {
-    if (tid == 0) {
-      float v = L[j * k + j];
-      const float ref = fabsf(G[0]) > 0.f ? fabsf(G[0]) : 1.f;
-      if (!(v > 1e-12f * ref)) v = 1e-12f * ref;
-      L[j * k + j] = sqrtf(v);
+// ONE wave, everything in registers, loops fully unrolled over KP so that every
+// register index is static: lane c holds column c of the trailing matrix
+// (right-looking Cholesky; the pivot row is broadcast with v_readlane), then
+// column c of X = L^-1 (forward substitution, L's rows broadcast the same way).
+// No LDS, no barriers: the former 256-thread version spent 48.6 us (config 4,
+// k = 32) in barrier-separated steps and an LDS-latency-bound inverse.
+__device__ __forceinline__ float lane_bcast(float v, int src) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
+}
+
+template <int KP>
+__global__ __launch_bounds__(64) void chol_rinv_kernel(const float* __restrict__ G, int k, int kp,
+                                                       float* __restrict__ Rinv) {
+  const int c = threadIdx.x;  // column owned by this lane
+  const bool live = c < k;
+  float A[KP];
+#pragma unroll
+  for (int i = 0; i < KP; ++i) A[i] = (live && i < k) ? G[i * kp + c] : 0.f;
+  const float ref0 = fabsf(lane_bcast(A[0], 0)) > 0.f ? fabsf(lane_bcast(A[0], 0)) : 1.f;
+  float dinv[KP];  // 1 / L[j][j], uniform
+  // Right-looking Cholesky: after step j, A[j] (lane c) = L[c][j] for c >= j.
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    if (j < k) {
+      float v = lane_bcast(A[j], j);
+      if (!(v > 1e-12f * ref0)) v = 1e-12f * ref0;
+      const float ljj = sqrtf(v);
+      dinv[j] = 1.0f / ljj;
+      const float l = (c == j) ? ljj : (c > j ? A[j] * dinv[j] : 0.f);
+      A[j] = l;
+#pragma unroll
+      for (int i = j + 1; i < KP; ++i)
+        if (i < k) A[i] = fmaf(-lane_bcast(l, i), l, A[i]);  // A[i][c] -= L[i][j] L[c][j]
+    } else {
+      dinv[j] = 0.f;
     }
-    __syncthreads();
-    const float inv = 1.0f / L[j * k + j];
-    for (int i = j + 1 + tid; i < k; i += 256) L[i * k + j] *= inv;
-    __syncthreads();
-    const int n = k - j - 1;
-    for (int idx = tid; idx < n * n; idx += 256) {
-      const int i = j + 1 + idx / n, c = j + 1 + idx % n;
-      if (c <= i) L[i * k + c] -= L[i * k + j] * L[c * k + j];
-    }
-    __syncthreads();
   }
-  for (int i = 0; i < k; ++i) {
-    const float inv = 1.0f / L[i * k + i];
-    for (int c = tid; c <= i; c += 256) {
+  // Lane r now holds row r of L in A[0 .. r].  X = L^-1 column c: for i = 0..k-1,
+  // X[i] = (delta_ic - sum_{t < i} L[i][t] X[t]) / L[i][i].
+  float X[KP];
+#pragma unroll
+  for (int i = 0; i < KP; ++i) {
+    if (i < k) {
       float s = (c == i) ? 1.0f : 0.0f;
-      for (int t = c; t < i; ++t) s -= L[i * k + t] * Li[t * k + c];
-      Li[i * k + c] = s * inv;
+#pragma unroll
+      for (int t = 0; t < i; ++t) s = fmaf(-lane_bcast(A[t], i), X[t], s);
+      X[i] = s * dinv[i];
+    } else {
+      X[i] = 0.f;
     }
-    __syncthreads();
   }
-  for (int idx = tid; idx < kp * kp; idx += 256) {
-    const int a = idx / kp, b = idx - a * kp;
-    Rinv[idx] = (a < k && b < k) ? Li[b * k + a] : 0.f;
+  // Rinv = L^-T: Rinv[c][i] = X[i][c] (lane c); rows / columns >= k are zero.
+  if (c < kp) {
+#pragma unroll
+    for (int i = 0; i < KP; ++i)
+      if (i < kp) Rinv[c * kp + i] = (live && i < k) ? X[i] : 0.f;
   }
+}
+
+void launch_chol_rinv(const float* G, int k, int kp, float* Rinv, hipStream_t st) {
+  if (kp <= 16)
+    hipLaunchKernelGGL(chol_rinv_kernel<16>, dim3(1), dim3(64), 0, st, G, k, kp, Rinv);
+  else if (kp <= 32)
+    hipLaunchKernelGGL(chol_rinv_kernel<32>, dim3(1), dim3(64), 0, st, G, k, kp, Rinv);
+  else if (kp <= 48)
+    hipLaunchKernelGGL(chol_rinv_kernel<48>, dim3(1), dim3(64), 0, st, G, k, kp, Rinv);
+  else
+    hipLaunchKernelGGL(chol_rinv_kernel<64>, dim3(1), dim3(64), 0, st, G, k, kp, Rinv);
 }
 
 struct OjaWs {
@@ -109,7 +135,7 @@ int cholqr2(const OjaWs& o, int64_t d, int k, int kp, hipStream_t st) {
     if ((rc = skinny_launch(true, cur, kp, cur, kp, o.G, kp, kp, kp, d, 1.f, 0.f, o.slab,
                             o.slab_bytes, st)))
       return rc;
-    hipLaunchKernelGGL(chol_rinv_kernel, dim3(1), dim3(256), 0, st, o.G, k, kp, o.Rinv);
+    launch_chol_rinv(o.G, k, kp, o.Rinv, st);
     DEIG_HIP_CHECK(hipGetLastError());
     if ((rc = skinny_launch(false, cur, kp, o.Rinv, kp, nxt, kp, d, kp, kp, 1.f, 0.f, o.slab,
                             o.slab_bytes, st)))
