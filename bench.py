@@ -326,8 +326,11 @@ def run_oneshot(args, cfg, world, rank, dev):
 
     if rank != 0:
         return None
+    # HBM-side bytes per covariance launch from the separate rocprofv3 PMC passes
+    # (FETCH_SIZE / WRITE_SIZE, gfx950 corrections; tools/profile_round.sh) of this
+    # same kernel and shard: tools/ travels to the GPU box, profiles/ does not.
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", f"pmc_syrk_{args.config}_{algo}.json")
+    pmc = os.path.join(ROOT, "tools", f"pmc_syrk_{args.config}_{algo}.json")
     if os.path.exists(pmc) and not args.rows:
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
@@ -347,7 +350,12 @@ def run_oneshot(args, cfg, world, rank, dev):
                           "residuals")
     line["roofline"] = {"bound": "mfma", "kernel": kernel, "achieved": achieved / 1e12,
                         "peak": peak / 1e12, "unit": "TFLOP/s", "frac": achieved / peak,
-                        "traffic": traffic, "algorithmic": algorithmic, "launch_ms": syrk_ms,
+                        "traffic": traffic,
+                        "traffic_source": (f"tools/pmc_syrk_{args.config}_{algo}.json (rocprofv3 "
+                                           "FETCH_SIZE x2 + WRITE_SIZE, separate passes; "
+                                           "fabric-side L2 misses incl. Infinity-Cache hits: an "
+                                           "upper bound on HBM bytes)") if traffic else None,
+                        "algorithmic": algorithmic, "launch_ms": syrk_ms,
                         "fp32_equiv_tflops": flops / (syrk_ms * 1e-3) / 1e12,
                         "fp32_mfma_peak": FP32_MFMA_PEAK / 1e12, "fp32_kernel": fp32_kernel}
     line["sweep"] = sweep
