@@ -28,6 +28,7 @@ DEIG_SWEEP_AUTO = 0
 DEIG_SWEEP_BF16X6 = 1
 DEIG_SWEEP_FP32 = 2
 DEIG_SWEEP_PREPARED = 0x100
+DEIG_SWEEP_ROUND_Q = 0x200
 SWEEP_ALGOS = {"auto": DEIG_SWEEP_AUTO, "bf16x6": DEIG_SWEEP_BF16X6, "fp32": DEIG_SWEEP_FP32}
 
 _c_i64 = ctypes.c_int64

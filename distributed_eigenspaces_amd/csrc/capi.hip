@@ -116,13 +116,15 @@ SolverWs carve_solver(void* ws, size_t cap, int64_t d, int k, int p, int64_t mk,
   return w;
 }
 
-int apply_op(const Operator& op, const SolverWs& w, int64_t d, int p, hipStream_t st) {
+int apply_op(const Operator& op, const SolverWs& w, int64_t d, int p, hipStream_t st,
+             bool round_q) {
   float* Q = w.rr.Z;
   float* Y = w.rr.Z + p;
   const int64_t ld = 2 * p;
   if (!op.implicit) {
     if (w.sweep_ws)
-      return sweep_apply(op.S, d, op.lds, Q, p, ld, Y, ld, 1.f, w.sweep_ws, w.sweep_bytes, st);
+      return sweep_apply(op.S, d, op.lds, Q, p, ld, Y, ld, 1.f, w.sweep_ws, w.sweep_bytes, st,
+                         round_q);
     return skinny_launch(true, op.S, op.lds, Q, ld, Y, ld, d, p, d, 1.f, 0.f, w.slab,
                          w.slab_bytes, st);
   }
@@ -175,8 +177,16 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
   int it = 0;
   float last = 3.4e38f;
   bool converged = false;
+  // Sweeps round Q to two bf16 pieces (five products instead of six, sweep.hip
+  // split_q_kernel) while the residual is above round_until: the rounding puts
+  // ~4e-6 relative noise into the basis each sweep, harmless while the Ritz
+  // vectors are far from converged, but a floor under the residual, so the
+  // closing sweeps use the exact (3-piece) Q.
+  static const float round_until =
+      getenv("DEIG_SWEEP_ROUND_UNTIL") ? (float)atof(getenv("DEIG_SWEEP_ROUND_UNTIL")) : 1e-4f;
   for (it = 0; it < max_sweeps; ++it) {
-    if ((rc = apply_op(op, w, d, p, st))) return rc;
+    const bool round_q = last > fmaxf(round_until, tol);
+    if ((rc = apply_op(op, w, d, p, st, round_q))) return rc;
     if (it > 0 && ++since_rr < rr_every && it + 1 < max_sweeps) {
       // power step on the live Ritz columns of the last RR (Q_j <- Y_j / ||Y w_j||)
       if ((rc = rr_power_launch(w.rr, d, p, tau, st))) return rc;
@@ -320,6 +330,7 @@ int deig_projavg_topk_f32(const float* Wt, int64_t d, int64_t mk, int64_t ldw, f
 }
 
 size_t deig_sym_apply_workspace(int64_t d, int p, int algo) {
+  algo &= ~(DEIG_SWEEP_PREPARED | DEIG_SWEEP_ROUND_Q);
   if (algo == DEIG_SWEEP_FP32) return skinny_workspace_bytes(d, p, d);
   return sweep_workspace_bytes(d, p);
 }
@@ -332,14 +343,16 @@ int deig_sym_apply_f32(const float* S, int64_t d, int64_t lds, const float* Q, i
     return skinny_launch(true, S, lds, Q, ldq, Y, ldy, d, p, d, alpha, 0.f,
                          static_cast<float*>(ws), ws_bytes, (hipStream_t)stream);
   const bool prepared = (algo & DEIG_SWEEP_PREPARED) != 0;
-  algo &= ~DEIG_SWEEP_PREPARED;
+  const bool round_q = (algo & DEIG_SWEEP_ROUND_Q) != 0;
+  algo &= ~(DEIG_SWEEP_PREPARED | DEIG_SWEEP_ROUND_Q);
   if (algo != DEIG_SWEEP_AUTO && algo != DEIG_SWEEP_BF16X6)
     return fail(DEIG_EINVAL, "sym_apply: unknown algorithm %d", algo);
   if (!prepared) {
     const int rc = sweep_prepare(S, d, lds, p, ws, ws_bytes, (hipStream_t)stream);
     if (rc) return rc;
   }
-  return sweep_apply(S, d, lds, Q, p, ldq, Y, ldy, alpha, ws, ws_bytes, (hipStream_t)stream);
+  return sweep_apply(S, d, lds, Q, p, ldq, Y, ldy, alpha, ws, ws_bytes, (hipStream_t)stream,
+                     round_q);
 }
 
 size_t deig_oja_workspace(int64_t b, int64_t d, int k) { return oja_workspace_bytes(b, d, k); }

@@ -92,8 +92,12 @@ int sweep_launch(const float* S, int64_t d, int64_t lds, const float* Q, int p, 
 // reads it in place).
 int sweep_prepare(const float* S, int64_t d, int64_t lds, int p, void* ws, size_t ws_bytes,
                   hipStream_t st);
+// round_q: the solver's in-place mode - Q (which must then be writable) is
+// rounded to 16 significant bits (Q' = h + m, two bf16 pieces) and the product
+// S Q' formed with five bf16 products instead of six (sweep.hip split_q_kernel).
 int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
-                float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st);
+                float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st,
+                bool round_q = false);
 
 // Rayleigh-Ritz pieces (rr.hip).
 struct RRBuffers {

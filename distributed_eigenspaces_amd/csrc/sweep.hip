@@ -81,10 +81,18 @@ __device__ __forceinline__ f32x4 mfma16(const u32x4& a, const u32x4& b, const f3
                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
 
-// Q (d x p, row stride ldq) -> image [k-group g = k/32][n-block j][h|m|l][lane][16 B],
+// Q (d x p, row stride ldq) -> image [k-group g = k/32][n-block j][piece][lane][16 B],
 // lane l of (g, j) holding Q[32 g + 8 (l/16) + e][16 j + l%16], e = 0..7; k-groups
 // beyond d are zeros.  One thread per (g, j, lane).
-__global__ __launch_bounds__(256) void split_q_kernel(const float* __restrict__ Q, int64_t ldq,
+// NP = 3: pieces h|m|l, Q represented to 2^-27 (the exact product, Q read-only).
+// NP = 2 (the solver's in-place mode): pieces h|m, and Q itself is rounded to
+// Q' = h + m (exact in fp32: 17 significant bits at most) and written back, so
+// the sweep computes S Q' to fp32 grade with five products (the dropped l*m term
+// is ~2^-24) and the Gram / Rayleigh-Ritz that follow see the same Q'.  The
+// solver only needs Y = S Q for the basis it holds; a 2^-17 perturbation of
+// that basis changes nothing it reports (the generalised RR accepts any Q).
+template <int NP>
+__global__ __launch_bounds__(256) void split_q_kernel(float* __restrict__ Q, int64_t ldq,
                                                       int64_t d, int nb, int64_t ngrp,
                                                       u32x4* __restrict__ QS) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -100,9 +108,18 @@ __global__ __launch_bounds__(256) void split_q_kernel(const float* __restrict__ 
   for (int e = 0; e < 8; ++e) v[e] = (k0 + e < d) ? Q[(k0 + e) * ldq + n] : 0.f;
   u32x4 hi, mi, lo;
   split8(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, hi, mi, lo);
-  QS[(t * 3 + 0) * 64 + lane] = hi;
-  QS[(t * 3 + 1) * 64 + lane] = mi;
-  QS[(t * 3 + 2) * 64 + lane] = lo;
+  QS[(t * NP + 0) * 64 + lane] = hi;
+  QS[(t * NP + 1) * 64 + lane] = mi;
+  if constexpr (NP == 3) {
+    QS[(t * NP + 2) * 64 + lane] = lo;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t k = k0 + 2 * q;
+      if (k < d) Q[k * ldq + n] = lo_f(hi[q]) + lo_f(mi[q]);
+      if (k + 1 < d) Q[(k + 1) * ldq + n] = hi_f(hi[q]) + hi_f(mi[q]);
+    }
+  }
 }
 
 template <int NB>
@@ -260,6 +277,31 @@ __global__ __launch_bounds__(SW_THR) void sweep_kernel(const float* __restrict__
       }
 }
 
+// The products of one Q fragment (pieces bh, bm[, bl]) with MB split S
+// fragments into column block j, small terms first, MB independent accumulators
+// between dependent MFMAs.  NP = 3: hh + hm + mh + hl + lh + mm (six); NP = 2
+// (Q = bh + bm exactly): hh + hm + mh + mm + lh (five; bl unused).
+template <int MB, int NP, int NB>
+__device__ __forceinline__ void sweep_products(f32x4 (&acc)[MB][NB], int j, const u32x4 (&ah)[MB],
+                                               const u32x4 (&am)[MB], const u32x4 (&al)[MB],
+                                               const u32x4& bh, const u32x4& bm,
+                                               const u32x4& bl) {
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(am[mb], bm, acc[mb][j]);
+  if constexpr (NP == 3) {
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bl, acc[mb][j]);
+  }
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(al[mb], bh, acc[mb][j]);
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bm, acc[mb][j]);
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(am[mb], bh, acc[mb][j]);
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bh, acc[mb][j]);
+}
+
 // ---------------------------------------------------------------- sweep v2
 // S image: S re-laid once per solve (sweep_prepare_kernel) in MFMA A-operand
 // order so that every wave streams one contiguous run of HBM:
@@ -324,7 +366,7 @@ __global__ __launch_bounds__(256) void sweep_prepare_kernel(const float* __restr
 // independently, each with a D-deep register ring of S and Q fragments.
 // PROBE (diagnostic builds only, DEIG_SWEEP_PROBE): bit 0 drops the MFMAs, bit 1
 // the S loads, bit 2 the Q loads (results are then garbage).
-template <int NB, int PROBE = 0>
+template <int NB, int NP, int PROBE = 0>
 __global__ __launch_bounds__(256, 1) void sweep2_kernel(const f32x4* __restrict__ SI, int64_t d,
                                                         const u32x4* __restrict__ QS,
                                                         int64_t ngrp, float* __restrict__ Y,
@@ -354,7 +396,7 @@ __global__ __launch_bounds__(256, 1) void sweep2_kernel(const f32x4* __restrict_
   // the split of group g + 1 fills the other, interleaved with them).
   const f32x4* sw = SI + rb * ngrp * (MB * 2 * 64) + lane;
   f32x4 sr[3][MB][2];
-  u32x4 qf[2][NB][3];
+  u32x4 qf[2][NB][NP];
   u32x4 pc[2][3][MB];
   auto clampg = [&](int64_t g) { return g < c1 ? g : c1 - 1; };
   auto load_s = [&](int b, int64_t g) {
@@ -370,15 +412,15 @@ __global__ __launch_bounds__(256, 1) void sweep2_kernel(const f32x4* __restrict_
       }
   };
   auto load_q = [&](int b, int64_t g) {
-    const u32x4* qg = QS + clampg(g) * (NB * 3 * 64) + lane;
+    const u32x4* qg = QS + clampg(g) * (NB * NP * 64) + lane;
 #pragma unroll
     for (int j = 0; j < NB; ++j)
 #pragma unroll
-      for (int p3 = 0; p3 < 3; ++p3) {
+      for (int p3 = 0; p3 < NP; ++p3) {
         if constexpr (PROBE & 4)
           qf[b][j][p3] = u32x4{(unsigned)g, (unsigned)j, (unsigned)p3, (unsigned)lane};
         else
-          qf[b][j][p3] = qg[(j * 3 + p3) * 64];
+          qf[b][j][p3] = qg[(j * NP + p3) * 64];
       }
   };
   auto split_into = [&](int ps, int b) {
@@ -396,26 +438,14 @@ __global__ __launch_bounds__(256, 1) void sweep2_kernel(const f32x4* __restrict_
     split_into(QB ^ 1, SB1);
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      const u32x4 bh = qf[QB][j][0], bm = qf[QB][j][1], bl = qf[QB][j][2];
+      const u32x4 bh = qf[QB][j][0], bm = qf[QB][j][1], bl = qf[QB][j][NP - 1];
       if constexpr (PROBE & 1) {
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb)
           acc[mb][j][0] += __uint_as_float((ah[mb][0] ^ am[mb][1] ^ al[mb][2] ^ bh[0] ^ bm[1] ^ bl[2]) & 0x3fffffffu);
         continue;
       }
-      // small terms first; MB independent accumulators between dependent MFMAs
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(am[mb], bm, acc[mb][j]);
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bl, acc[mb][j]);
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(al[mb], bh, acc[mb][j]);
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bm, acc[mb][j]);
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(am[mb], bh, acc[mb][j]);
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bh, acc[mb][j]);
+      sweep_products<MB, NP>(acc, j, ah, am, al, bh, bm, bl);
     }
     load_q(QB, g + 2);   // the Q slot just consumed
     load_s(SB1, g + 4);  // the S slot just split
@@ -491,14 +521,14 @@ __device__ __forceinline__ void sw_dma16(const __amdgpu_buffer_rsrc_t rsrc, int 
                : "memory", "m0");
 }
 
-template <int NB, int D>
-__global__ __launch_bounds__(256, 1) void sweep3_kernel(const f32x4* __restrict__ SI, int64_t d,
+template <int NB, int NP, int D, int OCC = 1>
+__global__ __launch_bounds__(256, OCC) void sweep3_kernel(const f32x4* __restrict__ SI, int64_t d,
                                                         const u32x4* __restrict__ QS,
                                                         int64_t ngrp, float* __restrict__ Y,
                                                         int64_t ldy, float alpha,
                                                         float* __restrict__ part) {
   constexpr int MB = 4;
-  constexpr int U = 3 * NB;          // 1-KiB Q pieces per k-group
+  constexpr int U = NP * NB;         // 1-KiB Q pieces per k-group
   constexpr int ND = (U + 3) / 4;    // DMAs per wave per group (tail pieces repeated)
   constexpr int SLOT = U * 1024;     // bytes per ring slot
   constexpr int NS = D + 1;          // ring slots
@@ -554,19 +584,9 @@ __global__ __launch_bounds__(256, 1) void sweep3_kernel(const f32x4* __restrict_
     const u32x4* qs = reinterpret_cast<const u32x4*>(qlds + (int)(g % NS) * SLOT) + lane;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      const u32x4 bh = qs[(j * 3 + 0) * 64], bm = qs[(j * 3 + 1) * 64], bl = qs[(j * 3 + 2) * 64];
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(am[mb], bm, acc[mb][j]);
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bl, acc[mb][j]);
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(al[mb], bh, acc[mb][j]);
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bm, acc[mb][j]);
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(am[mb], bh, acc[mb][j]);
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bh, acc[mb][j]);
+      const u32x4 bh = qs[(j * NP + 0) * 64], bm = qs[(j * NP + 1) * 64];
+      const u32x4 bl = qs[(j * NP + NP - 1) * 64];
+      sweep_products<MB, NP>(acc, j, ah, am, al, bh, bm, bl);
     }
     // Refill D groups ahead (clamped: the tail re-loads the last group into its
     // own slot, which holds the same bytes, so no reader sees a change).
@@ -610,16 +630,20 @@ __global__ __launch_bounds__(256, 1) void sweep3_kernel(const f32x4* __restrict_
       }
 }
 
+// Slabs summed in slice order (deterministic), four columns per thread (p % 16
+// == 0; Y 16-byte aligned with ldy % 4 == 0, else one column per thread).
+template <int V>
 __global__ __launch_bounds__(256) void sweep_reduce_kernel(const float* __restrict__ part, int ks,
                                                            int64_t d, int p, float alpha,
                                                            float* __restrict__ Y, int64_t ldy) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  using fv = std::conditional_t<V == 1, float, f32x4>;
+  const int64_t idx = ((int64_t)blockIdx.x * 256 + threadIdx.x) * V;
   if (idx >= d * p) return;
   const int64_t m = idx / p;
   const int n = (int)(idx - m * p);
-  float s = 0.f;
-  for (int k = 0; k < ks; ++k) s += part[(int64_t)k * d * p + idx];
-  Y[m * ldy + n] = alpha * s;
+  fv s = *reinterpret_cast<const fv*>(part + idx);
+  for (int k = 1; k < ks; ++k) s += *reinterpret_cast<const fv*>(part + (int64_t)k * d * p + idx);
+  *reinterpret_cast<fv*>(Y + m * ldy + n) = alpha * s;
 }
 
 int sweep_bpc() {
@@ -664,17 +688,17 @@ void launch_v1(dim3 grid, hipStream_t st, const float* S, int64_t lds, int64_t d
                      Y, ldy, alpha, part);
 }
 
-template <int NB>
+template <int NB, int NP>
 void launch_v2(dim3 grid, hipStream_t st, const f32x4* SI, int64_t d, const u32x4* QS, float* Y,
                int64_t ldy, float alpha, float* part) {
   const int64_t ng = si_groups(d);
-  if constexpr (NB == 5) {
+  if constexpr (NB == 5 && NP == 3) {
     static const int probe = getenv("DEIG_SWEEP_PROBE") ? atoi(getenv("DEIG_SWEEP_PROBE")) : 0;
     switch (probe) {
 #define DEIG_PROBE_CASE(P_)                                                                   \
   case P_:                                                                                   \
-    hipLaunchKernelGGL((sweep2_kernel<NB, P_>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy, \
-                       alpha, part);                                                         \
+    hipLaunchKernelGGL((sweep2_kernel<NB, NP, P_>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, \
+                       ldy, alpha, part);                                                    \
     return;
       DEIG_PROBE_CASE(1) DEIG_PROBE_CASE(2) DEIG_PROBE_CASE(3) DEIG_PROBE_CASE(4)
       DEIG_PROBE_CASE(5) DEIG_PROBE_CASE(6) DEIG_PROBE_CASE(7)
@@ -682,24 +706,43 @@ void launch_v2(dim3 grid, hipStream_t st, const f32x4* SI, int64_t d, const u32x
       default: break;
     }
   }
-  hipLaunchKernelGGL((sweep2_kernel<NB>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy, alpha,
-                     part);
+  hipLaunchKernelGGL((sweep2_kernel<NB, NP>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy,
+                     alpha, part);
 }
 
-template <int NB>
+template <int NB, int NP>
 void launch_v3(dim3 grid, hipStream_t st, const f32x4* SI, int64_t d, const u32x4* QS, float* Y,
                int64_t ldy, float alpha, float* part) {
   static const int de = getenv("DEIG_SWEEP_DEPTH") ? atoi(getenv("DEIG_SWEEP_DEPTH")) : 3;
   const int64_t ng = si_groups(d);
   if (de == 4)
-    hipLaunchKernelGGL((sweep3_kernel<NB, 4>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy,
+    hipLaunchKernelGGL((sweep3_kernel<NB, NP, 4>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy,
                        alpha, part);
   else if (de == 2)
-    hipLaunchKernelGGL((sweep3_kernel<NB, 2>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy,
+    hipLaunchKernelGGL((sweep3_kernel<NB, NP, 2>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy,
                        alpha, part);
   else
-    hipLaunchKernelGGL((sweep3_kernel<NB, 3>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy,
+    hipLaunchKernelGGL((sweep3_kernel<NB, NP, 3>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy,
                        alpha, part);
+}
+
+// v2 (sweep3 = false) or v3 with NP Q pieces, NB = p / 16 column blocks.
+template <int NP>
+void launch_image(bool v3, int nb, dim3 grid, hipStream_t st, const f32x4* SI, int64_t d,
+                  const u32x4* QS, float* Y, int64_t ldy, float alpha, float* part) {
+#define DEIG_NB_CASE(N_)                                              \
+  case N_:                                                            \
+    if (v3)                                                           \
+      launch_v3<N_, NP>(grid, st, SI, d, QS, Y, ldy, alpha, part);    \
+    else                                                              \
+      launch_v2<N_, NP>(grid, st, SI, d, QS, Y, ldy, alpha, part);    \
+    return;
+  switch (nb) {
+    DEIG_NB_CASE(1) DEIG_NB_CASE(2) DEIG_NB_CASE(3) DEIG_NB_CASE(4)
+    DEIG_NB_CASE(5) DEIG_NB_CASE(6) DEIG_NB_CASE(7)
+    default: DEIG_NB_CASE(8)
+  }
+#undef DEIG_NB_CASE
 }
 
 // Workspace: [Q image][split-K slabs][S image (v2)].
@@ -744,8 +787,20 @@ int sweep_prepare(const float* S, int64_t d, int64_t lds, int p, void* ws, size_
   return DEIG_OK;
 }
 
+// Q pieces in round_q mode: 2 unless DEIG_SWEEP_QPIECES=3 (A/B: exact Q, six
+// products, Q left untouched).
+int sweep_round_pieces() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DEIG_SWEEP_QPIECES");
+    v = (e && atoi(e) == 3) ? 3 : 2;
+  }
+  return v;
+}
+
 int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
-                float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st) {
+                float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st,
+                bool round_q) {
   DEIG_REQUIRE(d >= 1 && p >= 16 && p <= 128 && p % 16 == 0,
                "sweep: need d >= 1 and p in {16, 32, ..., 128} (p=%d)", p);
   DEIG_REQUIRE(lds >= d && lds % 4 == 0 && lds <= (1 << 24) && ldq >= p && ldy >= p,
@@ -756,8 +811,15 @@ int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, i
     return fail(DEIG_EWORKSPACE, "sweep: workspace %zu < %zu", ws_bytes, w.total);
   const int nb = p / 16;
   const int64_t ngrp = 2 * cdiv(d, SW_KS);
-  hipLaunchKernelGGL(split_q_kernel, dim3((unsigned)cdiv(ngrp * nb * 64, 256)), dim3(256), 0, st,
-                     Q, ldq, d, nb, ngrp, w.QS);
+  // v1 reads the 3-piece image only.
+  const int np = (round_q && sweep_version() != 1) ? sweep_round_pieces() : 3;
+  const dim3 qgrid((unsigned)cdiv(ngrp * nb * 64, 256));
+  if (np == 2)
+    hipLaunchKernelGGL(split_q_kernel<2>, qgrid, dim3(256), 0, st, const_cast<float*>(Q), ldq, d,
+                       nb, ngrp, w.QS);
+  else
+    hipLaunchKernelGGL(split_q_kernel<3>, qgrid, dim3(256), 0, st, const_cast<float*>(Q), ldq, d,
+                       nb, ngrp, w.QS);
   DEIG_HIP_CHECK(hipGetLastError());
   const int ks = sweep_ks(d);
   const dim3 grid((unsigned)(cdiv(d, SW_ROWS) * ks));
@@ -772,33 +834,21 @@ int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, i
       case 7: launch_v1<7>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
       default: launch_v1<8>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
     }
-  } else if (sweep_version() == 3 || (sweep_version() == 0 && nb > 5)) {
-    switch (nb) {
-      case 1: launch_v3<1>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 2: launch_v3<2>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 3: launch_v3<3>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 4: launch_v3<4>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 5: launch_v3<5>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 6: launch_v3<6>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 7: launch_v3<7>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
-      default: launch_v3<8>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
-    }
   } else {
-    switch (nb) {
-      case 1: launch_v2<1>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 2: launch_v2<2>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 3: launch_v2<3>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 4: launch_v2<4>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 5: launch_v2<5>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 6: launch_v2<6>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 7: launch_v2<7>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
-      default: launch_v2<8>(grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part); break;
-    }
+    const bool v3 = sweep_version() == 3 || (sweep_version() == 0 && nb > 5);
+    if (np == 2)
+      launch_image<2>(v3, nb, grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part);
+    else
+      launch_image<3>(v3, nb, grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part);
   }
   DEIG_HIP_CHECK(hipGetLastError());
   if (ks > 1) {
-    hipLaunchKernelGGL(sweep_reduce_kernel, dim3((unsigned)cdiv(d * p, 256)), dim3(256), 0, st,
-                       w.part, ks, d, p, alpha, Y, ldy);
+    if (ldy % 4 == 0 && aligned16(Y))
+      hipLaunchKernelGGL(sweep_reduce_kernel<4>, dim3((unsigned)cdiv(d * p / 4, 256)), dim3(256),
+                         0, st, w.part, ks, d, p, alpha, Y, ldy);
+    else
+      hipLaunchKernelGGL(sweep_reduce_kernel<1>, dim3((unsigned)cdiv(d * p, 256)), dim3(256), 0,
+                         st, w.part, ks, d, p, alpha, Y, ldy);
     DEIG_HIP_CHECK(hipGetLastError());
   }
   return DEIG_OK;
@@ -808,7 +858,7 @@ int sweep_launch(const float* S, int64_t d, int64_t lds, const float* Q, int p, 
                  float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st) {
   int rc = sweep_prepare(S, d, lds, p, ws, ws_bytes, st);
   if (rc) return rc;
-  return sweep_apply(S, d, lds, Q, p, ldq, Y, ldy, alpha, ws, ws_bytes, st);
+  return sweep_apply(S, d, lds, Q, p, ldq, Y, ldy, alpha, ws, ws_bytes, st, false);
 }
 
 }  // namespace deig

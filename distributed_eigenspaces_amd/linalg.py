@@ -332,12 +332,16 @@ def oja_steps(X: torch.Tensor, V: torch.Tensor, eta: float, batch: int,
 
 # ---------------------------------------------------------------- sweep
 def sym_apply(S: torch.Tensor, Q: torch.Tensor, algo: str = "auto", alpha: float = 1.0,
-              out: torch.Tensor | None = None, prepared: bool = False) -> torch.Tensor:
+              out: torch.Tensor | None = None, prepared: bool = False,
+              round_q: bool = False) -> torch.Tensor:
     """Y = alpha * S Q for symmetric S (d x d) and Q (d x p, p % 16 == 0, p <= 128):
     one subspace-iteration sweep of ``topk_eigh`` (include/deig.h DEIG_SWEEP_*):
     algo "bf16x6" (default via "auto") or "fp32".  ``prepared=True`` (bf16x6) reuses
     the sweep image of S left in this stream's workspace by the previous call with
-    the same S and p (DEIG_SWEEP_PREPARED), as the solver does between sweeps."""
+    the same S and p (DEIG_SWEEP_PREPARED), as the solver does between sweeps.
+    ``round_q=True`` (bf16x6, the solver's mode, DEIG_SWEEP_ROUND_Q): Q (contiguous,
+    modified in place) is rounded to its two leading bf16 pieces and Y = alpha S Q'
+    is formed from five bf16 products."""
     if algo not in _lib.SWEEP_ALGOS:
         raise ValueError(f"algo must be one of {sorted(_lib.SWEEP_ALGOS)}, got {algo!r}")
     S = require_device_tensor(S, "sym_apply")
@@ -348,14 +352,20 @@ def sym_apply(S: torch.Tensor, Q: torch.Tensor, algo: str = "auto", alpha: float
     p = Q.shape[1]
     if d % 4 or S.stride(1) != 1 or S.stride(0) % 4 or S.data_ptr() % 16:
         raise ValueError("S must be row-major with d % 4 == 0 and a 16-byte aligned, %4 stride")
+    if round_q:
+        if algo == "fp32" or not Q.is_contiguous() or Q.dtype != torch.float32:
+            raise ValueError("round_q needs algo bf16x6/auto and a contiguous float32 Q "
+                             "(it is rounded in place)")
     Q = Q.contiguous()
     Y = out if out is not None else torch.empty((d, p), dtype=torch.float32, device=S.device)
     code = _lib.SWEEP_ALGOS[algo]
     if prepared and code != _lib.DEIG_SWEEP_FP32:
         code |= _lib.DEIG_SWEEP_PREPARED
+    if round_q:
+        code |= _lib.DEIG_SWEEP_ROUND_Q
     L = _lib.lib()
     with torch.cuda.device(S.device):
-        nbytes = L.deig_sym_apply_workspace(d, p, code & ~_lib.DEIG_SWEEP_PREPARED)
+        nbytes = L.deig_sym_apply_workspace(d, p, code)
         ws = _workspace(S.device, nbytes)
         rc = L.deig_sym_apply_f32(S.data_ptr(), d, S.stride(0), Q.data_ptr(), p, Q.stride(0),
                                   Y.data_ptr(), Y.stride(0), ctypes.c_float(alpha), code,

@@ -91,6 +91,11 @@ int deig_default_subspace(int64_t d, int k);
  * S, d, p and workspace, so the re-layout pass is skipped (repeated products
  * with one S, as the solver does). */
 #define DEIG_SWEEP_PREPARED 0x100
+/* OR-ed into the algorithm of deig_sym_apply_f32 (BF16X6 only): the solver's
+ * mode.  Q (then written in place) is rounded to Q' = h + m, its two leading
+ * bf16 pieces (16 significant bits, |Q' - Q| <= 2^-17 |Q|), and Y = alpha S Q'
+ * is formed to fp32 grade from five bf16 MFMA products instead of six. */
+#define DEIG_SWEEP_ROUND_Q 0x200
 
 /* One subspace-iteration sweep Y = alpha * S Q  (S symmetric d x d row-major, lds;
  * Q d x p row-major, ldq; Y d x p row-major, ldy; p % 16 == 0, 16 <= p <= 128).

@@ -224,6 +224,32 @@ def test_sym_apply_prepared_image_reuse(d, p, ld, cuda):
         assert err <= 2e-6, f"prepared sweep {it}: rel err {err:.3e}"
 
 
+@pytest.mark.parametrize("d,p", [(520, 80), (300, 128), (1000, 16), (8192, 80)])
+def test_sym_apply_round_q(d, p, cuda):
+    """The solver's mode (DEIG_SWEEP_ROUND_Q): Q is rounded in place to Q' = h + m
+    (two bf16 pieces: |Q' - Q| <= 2^-17 |Q|, Q' exactly bf16(Q') + bf16(Q' - bf16(Q'))),
+    and Y = S Q' to fp32 grade (five bf16 products) against float64 S @ Q'."""
+    import distributed_eigenspaces_amd as de
+    rng = np.random.default_rng(7 * d + p)
+    A = rng.standard_normal((d, d)).astype(np.float32)
+    S = ((A + A.T) * 0.5).astype(np.float32)
+    Q = rng.standard_normal((d, p)).astype(np.float32)
+    St = torch.from_numpy(S).to(cuda)
+    Qt = torch.from_numpy(Q).to(cuda)
+    for it in range(2):
+        Y = de.sym_apply(St, Qt, algo="bf16x6", prepared=it > 0, round_q=True)
+        Qr = Qt.cpu().numpy()
+        assert np.all(np.abs(Qr - Q) <= 2.0 ** -17 * np.abs(Q) * 1.0001), "rounding exceeds 2^-17"
+        h = torch.from_numpy(Qr).to(torch.bfloat16).float()
+        m = (torch.from_numpy(Qr) - h).to(torch.bfloat16).float()
+        assert torch.equal(h + m, torch.from_numpy(Qr)), "Q' is not two bf16 pieces"
+        ref = S.astype(np.float64) @ Qr.astype(np.float64)
+        err = np.abs(Y.cpu().numpy() - ref).max() / np.abs(ref).max()
+        assert err <= 2e-6, f"round_q sweep d={d} p={p} it={it}: rel err {err:.3e}"
+        # idempotent: Q' is already two pieces, a second sweep leaves it unchanged
+        Q = Qr
+
+
 def test_sym_apply_rejects_bad_p(cuda):
     import distributed_eigenspaces_amd as de
     S = torch.eye(64, device=cuda)

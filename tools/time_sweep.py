@@ -20,17 +20,26 @@ for d, p in cases:
     Q = torch.randn((d, p), generator=g, device=dev)
     Y = torch.empty((d, p), device=dev)
     ref = (S.double() @ Q.double())
-    for algo in ("bf16x6", "fp32"):
-        de.sym_apply(S, Q, algo=algo, out=Y)
+    for algo in ("bf16x6", "bf16x5", "fp32"):
+        rq = algo == "bf16x5"  # the solver's mode: Q rounded in place, five products
+        if rq:
+            algo, Q0 = "bf16x6", Q
+            Q = Q.clone()
+        de.sym_apply(S, Q, algo=algo, out=Y, round_q=rq)
+        if rq:
+            ref = S.double() @ Q.double()
         err = ((Y.double() - ref).abs().max() / ref.abs().max()).item()
         reps = 30
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
         for _ in range(reps):  # the solver's case: S image built once (bf16x6)
-            de.sym_apply(S, Q, algo=algo, out=Y, prepared=True)
+            de.sym_apply(S, Q, algo=algo, out=Y, prepared=True, round_q=rq)
         e1.record(st)
         e1.synchronize()
         us = e0.elapsed_time(e1) / reps * 1e3
+        if rq:
+            algo, Q = "bf16x5", Q0
+            ref = S.double() @ Q.double()
         print(f"d={d:6d} p={p:4d} {algo:7s} {us:9.1f} us  {4.0*d*d/us/1e3:8.1f} GB/s  "
               f"({4.0*d*d/us/1e3/8000*100:5.1f}% of 8 TB/s)  max rel err {err:.2e}", flush=True)
     del S, Q, Y, ref
