@@ -201,10 +201,13 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
     DEIG_HIP_CHECK(hipMemcpyAsync(&last, w.rr.resid + k, sizeof(float), hipMemcpyDeviceToHost, st));
     DEIG_HIP_CHECK(hipStreamSynchronize(st));
     if (debug) {
-      int inf[3] = {0, 0, 0};
+      int inf[9] = {0};
       DEIG_HIP_CHECK(hipMemcpy(inf, w.rr.info, sizeof(inf), hipMemcpyDeviceToHost));
-      fprintf(stderr, "[deig] d=%lld k=%d p=%d sweep %d resid %.3e chol_floor %d jacobi_sweeps %d rotations %d\n",
-              (long long)d, k, p, it + 1, last, inf[0], inf[1], inf[2]);
+      fprintf(stderr, "[deig] d=%lld k=%d p=%d sweep %d resid %.3e chol_floor %d jacobi_sweeps %d rotations %d"
+              " small-solve us: chol %.1f linv %.1f congr %.1f jacobi %.1f tail %.1f\n",
+              (long long)d, k, p, it + 1, last, inf[0], inf[1], inf[2], inf[4] * 0.01,
+              (inf[5] - inf[4]) * 0.01, (inf[6] - inf[5]) * 0.01, (inf[7] - inf[6]) * 0.01,
+              (inf[8] - inf[7]) * 0.01);
     }
     if (!(last == last) || last > 3.0e38f) {  // NaN / Inf
       if (sweeps_out) *sweeps_out = it + 1;

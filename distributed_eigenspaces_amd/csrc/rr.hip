@@ -68,6 +68,38 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return red[RT / 64];
 }
 
+// C = A B for p x p row-major matrices in LDS (p % 4 == 0, p <= 128): thread tid
+// owns the 4 x 4 block at (a0, b0) and returns it in acc (false: no block).  Per
+// 4-wide k step: 4 + 4 ds_read_b128 for 64 FMAs into independent accumulators
+// (the former one-output-per-thread loops were LDS-latency-bound chains).
+__device__ __forceinline__ bool lds_gemm4(const float* A, const float* B, int p, int tid,
+                                          float (&acc)[4][4], int& a0, int& b0) {
+  const int nt = p >> 2;
+  const bool act = tid < nt * nt;
+  const int tr = act ? tid / nt : 0;
+  a0 = 4 * tr;
+  b0 = 4 * (tid - tr * nt);
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[r][c] = 0.f;
+  if (!act) return false;
+  for (int t = 0; t < p; t += 4) {
+    f32x4 ar[4], br[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ar[r] = *reinterpret_cast<const f32x4*>(A + (a0 + r) * p + t);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) br[u] = *reinterpret_cast<const f32x4*>(B + (t + u) * p + b0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(ar[r][u], br[u][c], acc[r][c]);
+  }
+  return true;
+}
+
 __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ Cg, int p,
                                                       float* __restrict__ Wout,
                                                       float* __restrict__ lam_out,
@@ -93,6 +125,11 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
   const float* Mg = Cg;
   const float* Hg = Cg + p;
   const float* Gg = Cg + (int64_t)p * ldc + p;
+  // Phase clock (100 MHz realtime counter) into info[4..8] for DEIG_DEBUG.
+  const uint64_t t0 = wall_clock64();
+  auto stamp = [&](int slot) {
+    if (tid == 0) info[slot] = (int)(wall_clock64() - t0);
+  };
 
   // ---- 0. D = diag(M)^-1/2;  X1 = D M D
   for (int a = tid; a < p; a += RT) {
@@ -111,84 +148,95 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
   }
   __syncthreads();
 
-  // ---- 1. Cholesky  D M D = L L^T  (lower, in place in X1), pivots floored
+  // Thread groups for the triangular steps: eight consecutive lanes per row
+  // (or column) split every dot product, reduced with three xor-shuffles.
+  const int grp = tid >> 3, part = tid & 7;
+  auto sum8 = [](float v) {
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    return v;
+  };
+
+  // ---- 1. Cholesky  D M D = L L^T  (left-looking, lower, in place in X1), pivots
+  //         floored.  Step j: group g finishes row i = j + g of column j from the
+  //         finished columns t < j - both dots split over its 8 lanes - and
+  //         recomputes the pivot itself, so one barrier per column.  The pivots
+  //         go to gd[] (X1's diagonal still holds D M D's, read by every group)
+  //         and onto the diagonal after the loop.
   for (int j = 0; j < p; ++j) {
-    if (tid == 0) {
-      float v = X1[j * p + j];
-      if (!(v > 1e-6f)) {
-        v = 1e-6f;
-        info[0] += 1;
+    const int i = j + grp;
+    if (i < p) {
+      float sd = 0.f, so = 0.f;
+      for (int t = part; t < j; t += 8) {
+        const float ljt = X1[j * p + t];
+        sd = fmaf(ljt, ljt, sd);
+        so = fmaf(X1[i * p + t], ljt, so);
       }
-      X1[j * p + j] = sqrtf(v);
-    }
-    __syncthreads();
-    const float inv = 1.0f / X1[j * p + j];
-    for (int i = j + 1 + tid; i < p; i += RT) X1[i * p + j] *= inv;
-    __syncthreads();
-    const int n = p - j - 1;
-    for (int idx = tid; idx < n * n; idx += RT) {
-      const int i = j + 1 + idx / n, c = j + 1 + idx % n;
-      if (c <= i) X1[i * p + c] -= X1[i * p + j] * X1[c * p + j];
+      sd = sum8(sd);
+      so = sum8(so);
+      float v = X1[j * p + j] - sd;
+      const bool floored = !(v > 1e-6f);
+      if (floored) v = 1e-6f;
+      const float ljj = sqrtf(v);
+      if (part == 0) {
+        if (i == j) {
+          gd[j] = ljj;
+          if (floored) info[0] += 1;
+        } else {
+          X1[i * p + j] = (X1[i * p + j] - so) / ljj;
+        }
+      }
     }
     __syncthreads();
   }
-
-  // ---- 2. L^-1 (lower) into X2, row by row
+  for (int a = tid; a < p; a += RT) X1[a * p + a] = gd[a];
   for (int idx = tid; idx < pp; idx += RT) X2[idx] = 0.f;
   __syncthreads();
+  stamp(4);
+
+  // ---- 2. L^-1 (lower) into X2, row by row; group c owns column c of row i,
+  //         its dot over t in [c, i) split over the group's 8 lanes.
   for (int i = 0; i < p; ++i) {
-    const float inv = 1.0f / X1[i * p + i];
-    for (int c = tid; c <= i; c += RT) {
-      float s = (c == i) ? 1.0f : 0.0f;
-      for (int t = c; t < i; ++t) s -= X1[i * p + t] * X2[t * p + c];
-      X2[i * p + c] = s * inv;
+    const int c = grp;
+    if (c <= i) {
+      float sacc = 0.f;
+      for (int t = c + part; t < i; t += 8) sacc = fmaf(X1[i * p + t], X2[t * p + c], sacc);
+      sacc = sum8(sacc);
+      if (part == 0) X2[i * p + c] = ((c == i ? 1.0f : 0.0f) - sacc) / X1[i * p + i];
     }
     __syncthreads();
   }
+  stamp(5);
 
-  // ---- 3. X1 = D H D ; 4. X1 = L^-1 X1 ; 5. X1 = X1 L^-T  (register-staged)
+  // ---- 3. X1 = D H D ; 4. T = L^-1 X1, stored transposed (X1 = T^T = X1^T L^-T);
+  //         5. X1 = L^-1 X1 = L^-1 H^T L^-T (symmetrised below: the same H~).
+  //         Register-blocked 4 x 4 products (lds_gemm4).
   for (int idx = tid; idx < pp; idx += RT) {
     const int a = idx / p, b = idx - a * p;
     X1[idx] = Hg[a * ldc + b] * dsc[a] * dsc[b];
   }
   __syncthreads();
-  float nv[16];
+  {
+    float acc[4][4];
+    int a0, b0;
+    bool act = lds_gemm4(X2, X1, p, tid, acc, a0, b0);
+    __syncthreads();
+    if (act)
 #pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int idx = tid + u * RT;
-    nv[u] = 0.f;
-    if (idx < pp) {
-      const int a = idx / p, b = idx - a * p;
-      float s = 0.f;
-      for (int t = 0; t <= a; ++t) s = fmaf(X2[a * p + t], X1[t * p + b], s);
-      nv[u] = s;
-    }
-  }
-  __syncthreads();
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int idx = tid + u * RT;
-    if (idx < pp) X1[idx] = nv[u];
-  }
-  __syncthreads();
+        for (int c = 0; c < 4; ++c) X1[(b0 + c) * p + a0 + r] = acc[r][c];
+    __syncthreads();
+    act = lds_gemm4(X2, X1, p, tid, acc, a0, b0);
+    __syncthreads();
+    if (act)
 #pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int idx = tid + u * RT;
-    nv[u] = 0.f;
-    if (idx < pp) {
-      const int a = idx / p, b = idx - a * p;
-      float s = 0.f;
-      for (int t = 0; t <= b; ++t) s = fmaf(X1[a * p + t], X2[b * p + t], s);
-      nv[u] = s;
-    }
-  }
-  __syncthreads();
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int idx = tid + u * RT;
-    if (idx < pp) X1[idx] = nv[u];
+        for (int c = 0; c < 4; ++c) X1[(a0 + r) * p + b0 + c] = acc[r][c];
+    __syncthreads();
   }
-  __syncthreads();
   // symmetrise H~ and turn X2 = L^-1 into the eigenvector accumulator V0 = L^-T:
   // every Jacobi rotation right-multiplies it, so at the end X2 = L^-T U.
   for (int idx = tid; idx < pp; idx += RT) {
@@ -204,6 +252,7 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
   }
   __syncthreads();
 
+  stamp(6);
   // ---- 6. parallel cyclic Jacobi on X1 (round-robin pairs; each thread owns a 2x2
   //         block of the rotated matrix, updated in place from one read).
   // nrot[0]: rotations in this sweep; nrot[1], nrot[2]: per-step counters used on
@@ -307,6 +356,7 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
     if (swrot == 0) break;
   }
 
+  stamp(7);
   // ---- 7. eigenvalues; W = D (L^-T U)  (row scaling, in place in X2)
   for (int a = tid; a < p; a += RT) lamv[a] = X1[a * p + a];
   __syncthreads();
@@ -316,25 +366,20 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
     X1[idx] = Gg[a * ldc + b];
   }
   __syncthreads();
-  // ---- 8. g_j = w_j^T G w_j
+  // ---- 8. g_j = w_j^T G w_j:  X1 = (G W) .* W, column sums below
+  {
+    float acc[4][4];
+    int a0, b0;
+    const bool act = lds_gemm4(X1, X2, p, tid, acc, a0, b0);
+    __syncthreads();
+    if (act)
 #pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int idx = tid + u * RT;
-    nv[u] = 0.f;
-    if (idx < pp) {
-      const int a = idx / p, j = idx - a * p;
-      float s = 0.f;
-      for (int b = 0; b < p; ++b) s = fmaf(X1[a * p + b], X2[b * p + j], s);
-      nv[u] = s * X2[idx];
-    }
-  }
-  __syncthreads();
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int idx = tid + u * RT;
-    if (idx < pp) X1[idx] = nv[u];
+        for (int c = 0; c < 4; ++c)
+          X1[(a0 + r) * p + b0 + c] = acc[r][c] * X2[(a0 + r) * p + b0 + c];
+    __syncthreads();
   }
-  __syncthreads();
   for (int j = tid; j < p; j += RT) {
     float s = 0.f;
     for (int a = 0; a < p; ++a) s += X1[a * p + j];
@@ -364,6 +409,7 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
     const int a = idx / p, j = idx - a * p;
     Wout[a * p + rank[j]] = X2[idx];
   }
+  stamp(8);
 }
 
 __global__ __launch_bounds__(256) void rr_update_kernel(float* __restrict__ Z, int64_t d, int p,
