@@ -113,11 +113,9 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
   float* dsc = X2 + pp;   // p
   float* lamv = dsc + p;  // p
   float* gd = lamv + p;   // p
-  float* pc = gd + p;     // p/2 rotation cosines
-  float* ps = pc + half;  // p/2 rotation sines
-  int* pa = reinterpret_cast<int*>(ps + half);  // p/2
-  int* pb = pa + half;                          // p/2
-  int* rank = pb + half;                        // p
+  // p/2 rotations {cos, sin, row a, row b} (16-byte aligned: p % 16 == 0)
+  f32x4* rotp = reinterpret_cast<f32x4*>(gd + p);
+  int* rank = reinterpret_cast<int*>(rotp + half);  // p
   float* red = reinterpret_cast<float*>(rank + p);  // RT/64 + 2
   int* nrot = reinterpret_cast<int*>(red + RT / 64 + 2);
   const int tid = threadIdx.x;
@@ -261,6 +259,9 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
     nrot[1] = 0;
     nrot[2] = 0;
   }
+  // idx = tid + u RT  ->  (idx / half, idx % half), stepped without divisions
+  const int tr0 = tid / half, tc0 = tid - tr0 * half;
+  const int dq = RT / half, dr = RT - dq * half;
   for (int sw = 0; sw < max_jsweeps; ++sw) {
     if (tid == 0) nrot[0] = 0;
     // scale for the absolute rotation threshold
@@ -311,15 +312,17 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
           s = t * c;
           atomicAdd(nrot + ci, 1);
         }
-        pa[tid] = a; pb[tid] = b; pc[tid] = c; ps[tid] = s;
+        rotp[tid] = f32x4{c, s, __int_as_float(a), __int_as_float(b)};
       }
       __syncthreads();
       const int step_rot = nrot[ci];
       if (step_rot != 0) {  // wave-uniform: identity steps apply nothing
+        int tr = tr0, tc = tc0;
         for (int idx = tid; idx < half * half; idx += RT) {
-          const int tr = idx / half, tc = idx - tr * half;
-          const int ar = pa[tr], br = pb[tr], ac = pa[tc], bc = pb[tc];
-          const float cr = pc[tr], sr = ps[tr], cc = pc[tc], sc = ps[tc];
+          const f32x4 qr = rotp[tr], qc = rotp[tc];
+          const int ar = __float_as_int(qr[2]), br = __float_as_int(qr[3]);
+          const int ac = __float_as_int(qc[2]), bc = __float_as_int(qc[3]);
+          const float cr = qr[0], sr = qr[1], cc = qc[0], sc = qc[1];
           const float x = X1[ar * p + ac], y = X1[ar * p + bc];
           const float z = X1[br * p + ac], w = X1[br * p + bc];
           // columns: col_a' = c col_a - s col_b ; col_b' = s col_a + c col_b
@@ -330,11 +333,26 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
           X1[br * p + ac] = sr * x1 + cr * z1;
           X1[ar * p + bc] = cr * y1 - sr * w1;
           X1[br * p + bc] = sr * y1 + cr * w1;
+          tr += dq;
+          tc += dr;
+          if (tc >= half) {
+            tc -= half;
+            ++tr;
+          }
         }
+        tr = tr0;
+        tc = tc0;
         for (int idx = tid; idx < p * half; idx += RT) {
-          const int r = idx / half, t = idx - r * half;
-          const int a = pa[t], b = pb[t];
-          const float c = pc[t], s = ps[t];
+          const int r = tr, t = tc;
+          tr += dq;
+          tc += dr;
+          if (tc >= half) {
+            tc -= half;
+            ++tr;
+          }
+          const f32x4 qt = rotp[t];
+          const int a = __float_as_int(qt[2]), b = __float_as_int(qt[3]);
+          const float c = qt[0], s = qt[1];
           const float va = X2[r * p + a], vb = X2[r * p + b];
           X2[r * p + a] = c * va - s * vb;
           X2[r * p + b] = s * va + c * vb;
@@ -533,7 +551,7 @@ int rr_init_launch(float* Z, int64_t d, int p, const float* Q0, int k0, int64_t 
 }
 
 int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream) {
-  DEIG_REQUIRE(p >= 2 && p <= 128 && p % 2 == 0, "rr_small: p=%d out of range", p);
+  DEIG_REQUIRE(p >= 4 && p <= 128 && p % 4 == 0, "rr_small: p=%d out of range", p);
   const size_t shm = rr_small_shm(p);
   static bool attr = false;
   if (!attr) {
