@@ -182,6 +182,10 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
   // ~4e-6 relative noise into the basis each sweep, harmless while the Ritz
   // vectors are far from converged, but a floor under the residual, so the
   // closing sweeps use the exact (3-piece) Q.
+  static const int jcap_sweeps =
+      getenv("DEIG_JACOBI_EARLY") ? atoi(getenv("DEIG_JACOBI_EARLY")) : 3;
+  static const float jcap_above =
+      getenv("DEIG_JACOBI_EARLY_ABOVE") ? (float)atof(getenv("DEIG_JACOBI_EARLY_ABOVE")) : 1e-2f;
   static const float round_until =
       getenv("DEIG_SWEEP_ROUND_UNTIL") ? (float)atof(getenv("DEIG_SWEEP_ROUND_UNTIL")) : 1e-4f;
   for (it = 0; it < max_sweeps; ++it) {
@@ -196,7 +200,12 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
     if ((rc = skinny_launch(true, w.rr.Z, 2 * p, w.rr.Z, 2 * p, w.rr.C, 2 * p, 2 * p, 2 * p, d,
                             1.f, 0.f, w.slab, w.slab_bytes, st)))
       return rc;
-    if ((rc = rr_small_launch(w.rr, p, st))) return rc;
+    // Early Rayleigh-Ritz steps (residual above jcap_above) run a capped number
+    // of Jacobi sweeps: the next basis Y W spans span(Y) for any invertible W, so
+    // subspace progress does not need converged Ritz vectors there; the residual
+    // of approximate pairs only over-states the error (no false convergence).
+    const int jcap = (jcap_sweeps > 0 && last > jcap_above) ? jcap_sweeps : 30;
+    if ((rc = rr_small_launch(w.rr, p, st, jcap))) return rc;
     if ((rc = rr_update_launch(w.rr, d, p, k, V, ldv, evals, st))) return rc;
     DEIG_HIP_CHECK(hipMemcpyAsync(&last, w.rr.resid + k, sizeof(float), hipMemcpyDeviceToHost, st));
     DEIG_HIP_CHECK(hipStreamSynchronize(st));

@@ -114,7 +114,8 @@ struct RRBuffers {
 };
 int rr_init_launch(float* Z, int64_t d, int p, const float* Q0, int k0, int64_t ldq0,
                    uint64_t seed, hipStream_t stream);
-int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream);
+// max_jsweeps caps the Jacobi sweeps of the small eigenproblem (30 = converge).
+int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream, int max_jsweeps = 30);
 int rr_update_blocks(int64_t d);
 int rr_power_launch(const RRBuffers& b, int64_t d, int p, float tau, hipStream_t stream);
 int rr_update_launch(const RRBuffers& b, int64_t d, int p, int k, float* V, int64_t ldv,

@@ -550,7 +550,7 @@ int rr_init_launch(float* Z, int64_t d, int p, const float* Q0, int k0, int64_t 
   return DEIG_OK;
 }
 
-int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream) {
+int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream, int max_jsweeps) {
   DEIG_REQUIRE(p >= 4 && p <= 128 && p % 4 == 0, "rr_small: p=%d out of range", p);
   const size_t shm = rr_small_shm(p);
   static bool attr = false;
@@ -561,7 +561,7 @@ int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream) {
     attr = true;
   }
   hipLaunchKernelGGL(rr_small_kernel, dim3(1), dim3(RT), shm, stream, b.C, p, b.W, b.lam, b.cs,
-                     b.info, 30);
+                     b.info, max_jsweeps);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }
