@@ -180,6 +180,7 @@ __global__ __launch_bounds__(256) void skinny_reduce_kernel(const float* __restr
   const int64_t m = idx / N;
   const int n = (int)(idx - m * N);
   fv s = *reinterpret_cast<const fv*>(part + idx);
+#pragma unroll 8
   for (int k = 1; k < ks; ++k) s += *reinterpret_cast<const fv*>(part + (int64_t)k * M * N + idx);
   fv* cp = reinterpret_cast<fv*>(C + m * ldc + n);
   const fv v = alpha * s;

@@ -642,6 +642,7 @@ __global__ __launch_bounds__(256) void sweep_reduce_kernel(const float* __restri
   const int64_t m = idx / p;
   const int n = (int)(idx - m * p);
   fv s = *reinterpret_cast<const fv*>(part + idx);
+#pragma unroll 8
   for (int k = 1; k < ks; ++k) s += *reinterpret_cast<const fv*>(part + (int64_t)k * d * p + idx);
   *reinterpret_cast<fv*>(Y + m * ldy + n) = alpha * s;
 }
