@@ -15,6 +15,23 @@ def test_header_symbols_exported():
         assert s in _lib.SIGNATURES, f"no ctypes signature for {s}"
 
 
+def test_header_constants_match_bindings():
+    """Every #define DEIG_<NAME> <int> in include/deig.h has the same value in _lib."""
+    import os
+    import re
+    hdr = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                       "deig.h")
+    defs = dict(re.findall(r"^#define\s+(DEIG_[A-Z0-9_]+)\s+\(?(-?(?:0x[0-9a-fA-F]+|\d+))\)?\s*$",
+                           open(hdr).read(), re.M))
+    assert "DEIG_SWEEP_ROUND_Q" in defs and "DEIG_SWEEP_PREPARED" in defs
+    checked = 0
+    for name, val in defs.items():
+        if hasattr(_lib, name):
+            assert getattr(_lib, name) == int(val, 0), f"{name}: header {val} != _lib"
+            checked += 1
+    assert checked >= 10
+
+
 def test_version_and_error_string():
     L = _lib.lib()
     assert L.deig_version() == 0x000100
