@@ -244,6 +244,7 @@ def run_oneshot(args, cfg, world, rank, dev):
     import distributed_eigenspaces_amd as de
     from distributed_eigenspaces_amd import synthetic
     from distributed_eigenspaces_amd.estimator import gather_bases
+    from distributed_eigenspaces_amd.my_threading import Slave
 
     n, d, k, W = cfg["rows"], cfg["d"], cfg["k"], cfg["workers"]
     if args.rows:
@@ -253,13 +254,66 @@ def run_oneshot(args, cfg, world, rank, dev):
     X = synthetic.spiked_samples(n, U, seed=1 + rank)
     S = torch.empty((d, d), dtype=torch.float32, device=dev)
     Wt_local = torch.empty((W * k, d), dtype=torch.float32, device=dev)
+    # W > 1 logical workers per GPU: each worker's eigensolve runs in its own
+    # my_threading.Slave thread on its own HIP stream, started as soon as its
+    # covariance is enqueued, so the latency-bound parts of one solve (the
+    # single-workgroup Rayleigh-Ritz step, host syncs) overlap the others' sweeps.
+    concurrent = W > 1 and not args.serial_workers
+    Ss = [S] + [torch.empty((d, d), dtype=torch.float32, device=dev)
+                for _ in range(W - 1)] if concurrent else None
+    side = [torch.cuda.Stream(dev) for _ in range(W)] if concurrent else None
     torch.cuda.synchronize()
     m = world * W
     stream = torch.cuda.current_stream(dev)
     rec = {"worker": [], "gather": [], "server": []}
     syrk_ev = []
 
+    def solve_on_side(w, ev):
+        with torch.cuda.stream(side[w]):
+            side[w].wait_event(ev)
+            r = de.topk_eigh(Ss[w], k, check_finite=False)  # synchronises side[w]
+            Wt_local[w * k:(w + 1) * k].copy_(r.V.t())
+            side[w].synchronize()
+        return r
+
+    def step_concurrent(record: bool):
+        t0 = time.perf_counter()
+        evs, slaves = [], []
+        for w in range(W):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            e[0].record(stream)
+            de.sigma_hat(X[w * ni:(w + 1) * ni], out=Ss[w], algo=args.syrk_algo)
+            e[1].record(stream)
+            sl = Slave(solve_on_side, w, e[1])
+            sl.start()
+            slaves.append((sl, e))
+        rs = []
+        for sl, e in slaves:
+            sl.join()
+            if sl.exception is not None:
+                raise sl.exception
+            rs.append(sl.result)
+            evs.append((e, sl.result.sweeps))
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        Wt = gather_bases(Wt_local)
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        res = None
+        if rank == 0:
+            res = de.projavg_topk(Wt, k, 1.0 / m, q0=Wt[:k].t())
+        torch.cuda.synchronize(dev)
+        t3 = time.perf_counter()
+        if record:
+            syrk_ev.extend(evs)
+            rec["worker"].append(t1 - t0)
+            rec["gather"].append(t2 - t1)
+            rec["server"].append(t3 - t2)
+        return rs[-1], res
+
     def step(record: bool):
+        if concurrent:
+            return step_concurrent(record)
         t0 = time.perf_counter()
         evs = []
         r = None
@@ -308,11 +362,15 @@ def run_oneshot(args, cfg, world, rank, dev):
     achieved = mfma_flops / (syrk_ms * 1e-3)
 
     # --- outside the timed region: accuracy, alternative kernel, sweep roofline
+    if concurrent:
+        del Ss[1:-1]  # keep worker 0's (S, reused below) and the last worker's buffer
+        torch.cuda.empty_cache()
     Xw = X[(W - 1) * ni:W * ni]
     cols = torch.randperm(d, generator=torch.Generator().manual_seed(7))[:16].to(dev)
     Xs = Xw.index_select(1, cols).double()
     S64 = (Xs.t() @ Xs) / ni
-    Sblk = S.index_select(0, cols).index_select(1, cols).double()
+    S_last = Ss[-1] if concurrent else S  # the last worker's covariance
+    Sblk = S_last.index_select(0, cols).index_select(1, cols).double()
     sigma_err = float((Sblk - S64).abs().max() / S64.abs().max())
     del Xs
     fp32_kernel = None
@@ -451,6 +509,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-alt", action="store_true", help="skip the fp32-kernel comparison launch")
+    ap.add_argument("--serial-workers", action="store_true",
+                    help="W > 1 workers per GPU: run each worker's solve after its covariance on "
+                         "one stream (default: solves in Slave threads on their own streams)")
     ap.add_argument("--syrk-algo", default="auto", choices=["auto", "split3", "fp32"])
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = rehearsal of the N>1 control flow with ranks sharing one GPU")
