@@ -79,9 +79,13 @@ def _gpu_worker(x: torch.Tensor, k: int, **kw):
 
 class DistributedEigenspaceEstimator:
     def __init__(self, k: int, workers_per_rank: int = 1, server_rank: int = 0, group=None,
-                 worker_fn=None, solver_kw=None):
+                 worker_fn=None, solver_kw=None, concurrent_workers: bool = False):
         self.k = int(k)
         self.wpr = int(workers_per_rank)
+        # concurrent_workers (default GPU worker, W > 1): covariances back to back on
+        # the caller's stream, each worker's eigensolve in a my_threading.Slave
+        # thread on its own HIP stream, chained by an event (bench.py's c5 mode).
+        self.concurrent = bool(concurrent_workers) and worker_fn is None
         self.server_rank = server_rank
         self.group = group
         self.worker_fn = worker_fn or _gpu_worker
@@ -95,12 +99,49 @@ class DistributedEigenspaceEstimator:
     def local_bases(self, X_local: torch.Tensor):
         """Run this rank's logical workers on contiguous pieces of X_local."""
         parts = shard_ranges(X_local.shape[0], self.wpr)
+        if self.concurrent and len(parts) > 1 and X_local.is_cuda:
+            return self._local_bases_concurrent(X_local, parts)
         rows, evs, sw = [], [], []
         for lo, hi in parts:
             V, ev, s = self.worker_fn(X_local[lo:hi], self.k, **self.solver_kw)
             rows.append(V.t())  # k x d view of the column-major basis
             evs.append(ev)
             sw.append(s)
+        return torch.cat(rows, dim=0).contiguous(), evs, sw
+
+    def _local_bases_concurrent(self, X_local: torch.Tensor, parts):
+        from .my_threading import Slave
+        dev = X_local.device
+        main = torch.cuda.current_stream(dev)
+        slaves = []
+        for lo, hi in parts:
+            S = linalg.sigma_hat(X_local[lo:hi])
+            ev = torch.cuda.Event()
+            ev.record(main)
+            st = torch.cuda.Stream(dev)
+            S.record_stream(st)
+
+            def solve(S=S, ev=ev, st=st):
+                with torch.cuda.stream(st):
+                    st.wait_event(ev)
+                    r = linalg.topk_eigh(S, self.k, check_finite=False, **self.solver_kw)
+                    st.synchronize()
+                return r
+
+            sl = Slave(solve)
+            sl.start()
+            slaves.append((sl, st))
+        rows, evs, sw = [], [], []
+        for sl, st in slaves:
+            sl.join()
+            if sl.exception is not None:
+                raise sl.exception
+            main.wait_stream(st)
+            r = sl.result
+            r.V.record_stream(main)
+            rows.append(r.V.t())
+            evs.append(r.evals)
+            sw.append(r.sweeps)
         return torch.cat(rows, dim=0).contiguous(), evs, sw
 
     def server(self, Wt: torch.Tensor, batches_number: int):

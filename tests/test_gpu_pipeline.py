@@ -155,6 +155,24 @@ def test_estimator_single_process(cuda):
     np.testing.assert_allclose(r.evals.cpu().numpy(), sw, rtol=EV_TOL)
 
 
+def test_estimator_concurrent_workers_match_serial(cuda):
+    """concurrent_workers=True (each worker's solve in a Slave thread on its own
+    stream, as bench.py runs config 5) gives the serial path's bases and the golden
+    server result."""
+    from distributed_eigenspaces_amd.estimator import DistributedEigenspaceEstimator
+    g = load_golden("spiked_d256_k10_m8")
+    X = torch.from_numpy(g["X"].astype(np.float32)).to(cuda)
+    k, m = int(g["k"]), int(g["m"])
+    rs = DistributedEigenspaceEstimator(k, workers_per_rank=m).fit(X)
+    rc = DistributedEigenspaceEstimator(k, workers_per_rank=m, concurrent_workers=True).fit(X)
+    torch.cuda.synchronize()
+    assert rc.sweeps_worker == rs.sweeps_worker
+    torch.testing.assert_close(rc.Wt, rs.Wt, rtol=0, atol=0)  # same kernels, same order
+    _, _, sw, sv = ref_cpu.one_shot(g["X"], k, m)
+    assert ref_cpu.projector_distance(rc.V.cpu().numpy(), sv) <= P_TOL
+    np.testing.assert_allclose(rc.evals.cpu().numpy(), sw, rtol=EV_TOL)
+
+
 def test_grayscale_ingest(cuda):
     from distributed_eigenspaces_amd import load_data
     rng = np.random.default_rng(0)
