@@ -50,6 +50,13 @@ int num_cus() {
 namespace {
 
 constexpr int kMaxP = 128;
+// Stagnation handling of the solver (see solve()): a stalled residual counts as
+// converged when <= max(kStallAcceptTol * tol, kStallAcceptAbs) - the fp32 floor
+// of ||S v - lambda v|| / |lambda_max| is a few 1e-7 up to d = 16384 - and the
+// solver gives up after kStallGiveUp Rayleigh-Ritz steps without a 10% gain.
+constexpr float kStallAcceptTol = 4.0f;
+constexpr float kStallAcceptAbs = 2e-6f;
+constexpr int kStallGiveUp = 12;
 
 struct Operator {
   bool implicit;
@@ -227,20 +234,31 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
       converged = true;
       break;
     }
-    // Stagnation at the fp32 floor: no 10% improvement for 4 sweeps.
+    // Stagnation: no 10% improvement over the best residual for 4 Rayleigh-Ritz
+    // steps in a row.  It counts as convergence only at the fp32 floor (residual
+    // within kStallAccept of tol); a stall above it is slow convergence (a small
+    // eigengap at k), so the iteration goes on and, if it stays stuck for
+    // kStallGiveUp RR steps, stops early with DEIG_NOT_CONVERGED.
     if (last < 0.9f * best) {
       best = last;
       since_best = 0;
     } else if (++since_best >= 4 && it >= 8) {
-      converged = true;
-      break;
+      if (last <= fmaxf(kStallAcceptTol * tol, kStallAcceptAbs)) {
+        converged = true;
+        break;
+      }
+      if (since_best >= kStallGiveUp) {
+        ++it;
+        break;
+      }
     }
   }
-  if (sweeps_out) *sweeps_out = converged ? it + 1 : max_sweeps;
+  if (sweeps_out) *sweeps_out = converged ? it + 1 : (it < max_sweeps ? it : max_sweeps);
   if (resid_out) *resid_out = last;
   if (!converged)
-    return fail(DEIG_NOT_CONVERGED, "solver: residual %g > tol %g after %d sweeps", last, tol,
-                max_sweeps);
+    return fail(DEIG_NOT_CONVERGED, "solver: residual %g > tol %g after %d sweeps%s", last, tol,
+                it < max_sweeps ? it : max_sweeps,
+                it < max_sweeps ? " (stalled: eigengap at k too small for the subspace)" : "");
   return DEIG_OK;
 }
 

@@ -114,31 +114,39 @@ class DistributedEigenspaceEstimator:
         dev = X_local.device
         main = torch.cuda.current_stream(dev)
         slaves = []
-        for lo, hi in parts:
-            S = linalg.sigma_hat(X_local[lo:hi])
-            ev = torch.cuda.Event()
-            ev.record(main)
-            st = torch.cuda.Stream(dev)
-            S.record_stream(st)
+        try:
+            for lo, hi in parts:
+                S = linalg.sigma_hat(X_local[lo:hi])
+                ev = torch.cuda.Event()
+                ev.record(main)
+                st = torch.cuda.Stream(dev)
+                S.record_stream(st)
 
-            def solve(S=S, ev=ev, st=st):
-                with torch.cuda.stream(st):
-                    st.wait_event(ev)
-                    r = linalg.topk_eigh(S, self.k, check_finite=False, **self.solver_kw)
-                    st.synchronize()
-                return r
+                def solve(S=S, ev=ev, st=st):
+                    with torch.cuda.stream(st):
+                        st.wait_event(ev)
+                        r = linalg.topk_eigh(S, self.k, check_finite=False, **self.solver_kw)
+                        st.synchronize()
+                    return r
 
-            sl = Slave(solve)
-            sl.start()
-            slaves.append((sl, st))
+                sl = Slave(solve)
+                sl.start()
+                slaves.append((sl, st))
+        finally:
+            # every started solve is joined before anything propagates (no orphaned
+            # threads still launching on their streams)
+            for sl, _ in slaves:
+                sl.join()
+        errors = [sl.exception for sl, _ in slaves if sl.exception is not None]
+        if errors:
+            raise errors[0]
         rows, evs, sw = [], [], []
         for sl, st in slaves:
-            sl.join()
-            if sl.exception is not None:
-                raise sl.exception
             main.wait_stream(st)
             r = sl.result
+            # both outputs were allocated on the side stream; the main stream reads them
             r.V.record_stream(main)
+            r.evals.record_stream(main)
             rows.append(r.V.t())
             evs.append(r.evals)
             sw.append(r.sweeps)
