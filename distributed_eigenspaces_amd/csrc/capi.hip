@@ -7,6 +7,8 @@
 #include <string.h>
 #include <math.h>
 
+#include <algorithm>
+
 #include "deig_internal.hpp"
 
 namespace deig {
@@ -70,6 +72,7 @@ struct Operator {
 struct SolverWs {
   RRBuffers rr;
   float* Zt;
+  float* T;  // d x p: X_{j-1} of the Chebyshev recurrence
   float* slab;
   size_t slab_bytes;
   void* sweep_ws;  // bf16x6 sweep (explicit S only)
@@ -101,6 +104,7 @@ SolverWs carve_solver(void* ws, size_t cap, int64_t d, int k, int p, int64_t mk,
   w.rr.resid = c.take<float>((size_t)k + 1);
   w.rr.info = c.take<int>(16);
   w.Zt = mk > 0 ? c.take<float>((size_t)mk * p) : nullptr;
+  w.T = c.take<float>((size_t)d * p);
   size_t sb = skinny_workspace_bytes(2 * p, 2 * p, d);  // Gram
   if (mk > 0) {
     const size_t a = skinny_workspace_bytes(mk, p, d);  // Wt Q
@@ -142,6 +146,54 @@ int apply_op(const Operator& op, const SolverWs& w, int64_t d, int p, hipStream_
                        w.slab_bytes, st);
 }
 
+// Chebyshev filter plan for the sweeps between two Rayleigh-Ritz steps (host side,
+// from the last RR's Ritz values theta_0 >= ... >= theta_{p-1} and residual).
+// The operator is assumed PSD (covariances, projector averages): the damped
+// interval is [0, c] with c = theta_{p-1} (the block's smallest Ritz value) when
+// the basis has guard columns, else min(theta_{p-1}, theta_{k-1} / 2).  Scaled
+// recurrence at gamma = theta_0 (Zhou & Saad): X_1 = (s1/e)(A - cc) X_0,
+// X_{j+1} = (2 s_{j+1}/e)(A - cc) X_j - s_j s_{j+1} X_{j-1}, s_{j+1} = 1/(2/s1 - s_j).
+// Degree m: at most kChebMaxDeg, at most what the residual still needs at column
+// k's damping rate, and small enough that a column's contamination by theta_0's
+// direction grows at most gmax = clamp(1/resid, 10, kChebGmax) times (the fp32
+// Gram of the filtered block must still resolve every column); columns whose
+// growth would exceed gmax stay out of the filter (threshold thr on theta_j).
+// Only used once resid <= kChebAbove: before that the Ritz values are too rough
+// to place the interval, and plain power steps run.
+constexpr float kChebAbove = 1e-2f;
+constexpr double kChebGmax = 1e4;
+constexpr int kChebMaxDeg = 16;
+
+struct ChebPlan {
+  int m = 0;
+  double cc = 0, e = 1, s1 = 0;
+  float thr = 0;
+};
+
+bool cheb_plan(const float* lam, int k, int p, float resid, float tol, ChebPlan* pl) {
+  if (!(resid <= kChebAbove) || !(resid > 0)) return false;
+  const double gmax = fmin(kChebGmax, fmax(10.0, 1.0 / (double)resid));
+  const double a = 0.0;
+  double c = lam[p - 1];
+  if (p - k < 4) c = fmin(c, 0.5 * (double)lam[k - 1]);
+  const double lk = lam[k - 1], l0 = lam[0];
+  if (!(lk > c && c > a && l0 > c)) return false;
+  const double cc = 0.5 * (c + a), e = 0.5 * (c - a);
+  const double tk = (lk - cc) / e, t0 = (l0 - cc) / e;
+  const double ak = acosh(tk), a0 = acosh(t0);
+  const double rho = 1.0 / (tk + sqrt(tk * tk - 1.0));  // column k's damping per degree
+  int m = kChebMaxDeg;
+  if (a0 - ak > 1e-9) m = std::min(m, std::max(1, (int)(log(gmax) / (a0 - ak))));
+  const double need = log(fmax(0.3 * (double)tol / (double)resid, 1e-30)) / log(rho);
+  m = std::max(1, std::min(m, (int)ceil(need)));
+  pl->m = m;
+  pl->cc = cc;
+  pl->e = e;
+  pl->s1 = 1.0 / t0;
+  pl->thr = (float)(cc + cosh(fmax(a0 - log(gmax) / m, 0.0)) * e);
+  return true;
+}
+
 int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol, const float* Q0,
           int k0, int64_t ldq0, float* V, int64_t ldv, float* evals, int* sweeps_out,
           float* resid_out, void* ws, size_t ws_bytes, hipStream_t st) {
@@ -160,17 +212,19 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
     return fail(DEIG_EWORKSPACE, "solver: workspace %zu bytes < required %zu", ws_bytes, total);
 
   static const bool debug = getenv("DEIG_DEBUG") && getenv("DEIG_DEBUG")[0] == '1';
-  // Rayleigh-Ritz (Gram + small solve + update + residual check) runs on every
-  // rr_every-th sweep; the sweeps between are plain power steps Q <- A Q on the
-  // Ritz vectors of the last RR (same span as subspace iteration; the
+  // Cycles: [filter / power sweeps] + one sweep with a Rayleigh-Ritz step (Gram +
+  // small solve + update + residual check).  Between two RRs either a Chebyshev
+  // filter of planned degree runs (cheb_plan; DEIG_CHEB=0 disables it) or, while
+  // the residual is above kChebAbove, rr_every - 1 plain power steps Q <- A Q on
+  // the Ritz vectors of the last RR (same span as subspace iteration; the
   // generalised RR copes with the non-orthonormal basis).  The single-workgroup
-  // small solve is the latency-bound part of a sweep, so this divides its cost.
-  // Every 4th sweep when the basis has >= 16 guard columns beyond k (measured:
-  // d=8192 k=64 p=80 6.2 vs 9.0 ms, d=3072 k=16 p=32 1.4 vs 1.9 ms); every 2nd
-  // without them (d=16384 k=128 p=128: 23 sweeps / 47 ms vs 41 / 54 ms), where
-  // the k-th column converges at lambda_{k+1}/lambda_k and extra power steps on
-  // the unconverged tail only delay the next re-orthogonalisation.
+  // small solve is the latency-bound part of a cycle, so spacing RRs divides its
+  // cost.  Power steps: every 4th sweep is an RR when the basis has >= 16 guard
+  // columns beyond k (measured: d=8192 k=64 p=80 6.2 vs 9.0 ms, d=3072 k=16 p=32
+  // 1.4 vs 1.9 ms); every 2nd without them (d=16384 k=128 p=128: 23 sweeps /
+  // 47 ms vs 41 / 54 ms).
   static const int rr_every_env = getenv("DEIG_RR_EVERY") ? atoi(getenv("DEIG_RR_EVERY")) : 0;
+  static const bool cheb_on = !(getenv("DEIG_CHEB") && getenv("DEIG_CHEB")[0] == '0');
   const int rr_every = rr_every_env > 0 ? rr_every_env : (p - k >= 16 ? 4 : 2);
   const float tau = rr_every > 1 ? powf(0.1f, 1.0f / (float)(rr_every - 1)) : 0.f;
   int rc = rr_init_launch(w.rr.Z, d, p, Q0, k0, ldq0, 0x5eed5eedull, st);
@@ -178,10 +232,11 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
   if (!op.implicit && w.sweep_ws &&
       (rc = sweep_prepare(op.S, d, op.lds, p, w.sweep_ws, w.sweep_bytes, st)))
     return rc;
+  float lam_h[kMaxP];
   float best = 3.4e38f;
   int since_best = 0;
-  int since_rr = 0;
-  int it = 0;
+  int it = 0;  // sweeps done
+  int nrr = 0;
   float last = 3.4e38f;
   bool converged = false;
   // Sweeps round Q to two bf16 pieces (five products instead of six, sweep.hip
@@ -195,15 +250,42 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
       getenv("DEIG_JACOBI_EARLY_ABOVE") ? (float)atof(getenv("DEIG_JACOBI_EARLY_ABOVE")) : 1e-2f;
   static const float round_until =
       getenv("DEIG_SWEEP_ROUND_UNTIL") ? (float)atof(getenv("DEIG_SWEEP_ROUND_UNTIL")) : 1e-4f;
-  for (it = 0; it < max_sweeps; ++it) {
+  while (it < max_sweeps) {
     const bool round_q = last > fmaxf(round_until, tol);
-    if ((rc = apply_op(op, w, d, p, st, round_q))) return rc;
-    if (it > 0 && ++since_rr < rr_every && it + 1 < max_sweeps) {
-      // power step on the live Ritz columns of the last RR (Q_j <- Y_j / ||Y w_j||)
-      if ((rc = rr_power_launch(w.rr, d, p, tau, st))) return rc;
-      continue;
+    ChebPlan plan;
+    const bool cheb = cheb_on && nrr > 0 && cheb_plan(lam_h, k, p, last, tol, &plan);
+    int ncheb = 0;
+    if (cheb) {
+      // degree j: apply A to X_j, then X_{j+1} from X_j, A X_j and X_{j-1}
+      const int m = std::min(plan.m, max_sweeps - it - 1);
+      double s_prev = plan.s1;
+      for (int j = 0; j < m; ++j, ++it) {
+        if ((rc = apply_op(op, w, d, p, st, round_q))) return rc;
+        double alpha, gamma;
+        if (j == 0) {
+          alpha = plan.s1 / plan.e;
+          gamma = 0.0;
+        } else {
+          const double s_next = 1.0 / (2.0 / plan.s1 - s_prev);
+          alpha = 2.0 * s_next / plan.e;
+          gamma = s_prev * s_next;
+          s_prev = s_next;
+        }
+        if ((rc = cheb_step_launch(w.rr, w.T, d, p, plan.thr, (float)alpha, (float)plan.cc,
+                                   (float)gamma, st)))
+          return rc;
+      }
+      ncheb = m;
+    } else if (nrr > 0) {
+      const int npow = std::min(rr_every - 1, max_sweeps - it - 1);
+      for (int j = 0; j < npow; ++j, ++it) {
+        if ((rc = apply_op(op, w, d, p, st, round_q))) return rc;
+        // power step on the live Ritz columns of the last RR (Q_j <- Y_j / ||Y w_j||)
+        if ((rc = rr_power_launch(w.rr, d, p, tau, st))) return rc;
+      }
     }
-    since_rr = 0;
+    if ((rc = apply_op(op, w, d, p, st, round_q))) return rc;
+    ++it;
     if ((rc = skinny_launch(true, w.rr.Z, 2 * p, w.rr.Z, 2 * p, w.rr.C, 2 * p, 2 * p, 2 * p, d,
                             1.f, 0.f, w.slab, w.slab_bytes, st)))
       return rc;
@@ -215,18 +297,21 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
     if ((rc = rr_small_launch(w.rr, p, st, jcap))) return rc;
     if ((rc = rr_update_launch(w.rr, d, p, k, V, ldv, evals, st))) return rc;
     DEIG_HIP_CHECK(hipMemcpyAsync(&last, w.rr.resid + k, sizeof(float), hipMemcpyDeviceToHost, st));
+    DEIG_HIP_CHECK(hipMemcpyAsync(lam_h, w.rr.lam, sizeof(float) * p, hipMemcpyDeviceToHost, st));
     DEIG_HIP_CHECK(hipStreamSynchronize(st));
+    ++nrr;
     if (debug) {
       int inf[9] = {0};
       DEIG_HIP_CHECK(hipMemcpy(inf, w.rr.info, sizeof(inf), hipMemcpyDeviceToHost));
-      fprintf(stderr, "[deig] d=%lld k=%d p=%d sweep %d resid %.3e chol_floor %d jacobi_sweeps %d rotations %d"
-              " small-solve us: chol %.1f linv %.1f congr %.1f jacobi %.1f tail %.1f\n",
-              (long long)d, k, p, it + 1, last, inf[0], inf[1], inf[2], inf[4] * 0.01,
+      fprintf(stderr, "[deig] d=%lld k=%d p=%d sweep %d resid %.3e cheb_deg %d chol_floor %d "
+              "jacobi_sweeps %d rotations %d small-solve us: chol %.1f linv %.1f congr %.1f "
+              "jacobi %.1f tail %.1f\n",
+              (long long)d, k, p, it, last, ncheb, inf[0], inf[1], inf[2], inf[4] * 0.01,
               (inf[5] - inf[4]) * 0.01, (inf[6] - inf[5]) * 0.01, (inf[7] - inf[6]) * 0.01,
               (inf[8] - inf[7]) * 0.01);
     }
     if (!(last == last) || last > 3.0e38f) {  // NaN / Inf
-      if (sweeps_out) *sweeps_out = it + 1;
+      if (sweeps_out) *sweeps_out = it;
       if (resid_out) *resid_out = last;
       return fail(DEIG_EINVAL, "solver: non-finite residual (input contains NaN/Inf?)");
     }
@@ -236,7 +321,7 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
     }
     // Stagnation: no 10% improvement over the best residual for 4 Rayleigh-Ritz
     // steps in a row.  It counts as convergence only at the fp32 floor (residual
-    // within kStallAccept of tol); a stall above it is slow convergence (a small
+    // within kStallAccept* of tol); a stall above it is slow convergence (a small
     // eigengap at k), so the iteration goes on and, if it stays stuck for
     // kStallGiveUp RR steps, stops early with DEIG_NOT_CONVERGED.
     if (last < 0.9f * best) {
@@ -247,18 +332,14 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
         converged = true;
         break;
       }
-      if (since_best >= kStallGiveUp) {
-        ++it;
-        break;
-      }
+      if (since_best >= kStallGiveUp) break;
     }
   }
-  if (sweeps_out) *sweeps_out = converged ? it + 1 : (it < max_sweeps ? it : max_sweeps);
+  if (sweeps_out) *sweeps_out = it;
   if (resid_out) *resid_out = last;
   if (!converged)
     return fail(DEIG_NOT_CONVERGED, "solver: residual %g > tol %g after %d sweeps%s", last, tol,
-                it < max_sweeps ? it : max_sweeps,
-                it < max_sweeps ? " (stalled: eigengap at k too small for the subspace)" : "");
+                it, it < max_sweeps ? " (stalled: eigengap at k too small for the subspace)" : "");
   return DEIG_OK;
 }
 

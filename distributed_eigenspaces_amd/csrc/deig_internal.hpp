@@ -118,6 +118,9 @@ int rr_init_launch(float* Z, int64_t d, int p, const float* Q0, int k0, int64_t 
 int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream, int max_jsweeps = 30);
 int rr_update_blocks(int64_t d);
 int rr_power_launch(const RRBuffers& b, int64_t d, int p, float tau, hipStream_t stream);
+// One scaled Chebyshev filter degree on Z = [X_j | A X_j] with T = X_{j-1} (d x p).
+int cheb_step_launch(const RRBuffers& b, float* T, int64_t d, int p, float thr, float alpha,
+                     float cc, float gamma, hipStream_t stream);
 int rr_update_launch(const RRBuffers& b, int64_t d, int p, int k, float* V, int64_t ldv,
                      float* evals, hipStream_t stream);
 

@@ -535,6 +535,38 @@ __global__ __launch_bounds__(256) void rr_power_kernel(float* __restrict__ Z, in
   if (c > 0.f && fabsf(lam[j]) >= tau * fabsf(lam[0])) Z[r * 2 * p + j] = Z[r * 2 * p + p + j] * c;
 }
 
+// One degree of the scaled Chebyshev filter between two Rayleigh-Ritz steps
+// (Zhou & Saad's scaled three-term recurrence; capi.hip plans alpha / cc / gamma
+// from the last RR's Ritz values).  Z = [X_j | A X_j] (ld 2p), T = X_{j-1} (ld p):
+//   X_{j+1} = alpha (A X_j - cc X_j) - gamma X_{j-1};  T <- X_j;  Z_q <- X_{j+1}
+// for the active columns (Ritz value >= thr); the others keep X_0 (like the weak
+// columns of rr_power_kernel: their contamination by the dominant directions
+// would grow past what the fp32 Gram resolves).  A column's recurrence is linear
+// in that column only, so per-column activation keeps every column a polynomial
+// in A of its start vector.  float4 over columns (p % 16 == 0).
+__global__ __launch_bounds__(256) void cheb_step_kernel(float* __restrict__ Z,
+                                                        float* __restrict__ T, int64_t d,
+                                                        int p, const float* __restrict__ lam,
+                                                        float thr, float alpha, float cc,
+                                                        float gamma) {
+  const int pq = p >> 2;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= d * pq) return;
+  const int64_t r = idx / pq;
+  const int j = (int)(idx - r * pq) * 4;
+  f32x4* zq = reinterpret_cast<f32x4*>(Z + r * 2 * p + j);
+  const f32x4 y = *reinterpret_cast<const f32x4*>(Z + r * 2 * p + p + j);
+  f32x4* tp = reinterpret_cast<f32x4*>(T + r * p + j);
+  const f32x4 q = *zq;
+  const f32x4 t = *tp;
+  f32x4 xn = q;
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (lam[j + u] >= thr) xn[u] = alpha * (y[u] - cc * q[u]) - gamma * t[u];
+  *tp = q;
+  *zq = xn;
+}
+
 size_t rr_small_shm(int p) {
   return (size_t)(2 * p * p + 6 * p + RT / 64 + 20) * sizeof(float);
 }
@@ -569,6 +601,15 @@ int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream, int max_jswee
 int rr_power_launch(const RRBuffers& b, int64_t d, int p, float tau, hipStream_t stream) {
   hipLaunchKernelGGL(rr_power_kernel, dim3((unsigned)cdiv(d * p, 256)), dim3(256), 0, stream, b.Z,
                      d, p, b.cs, b.lam, tau);
+  DEIG_HIP_CHECK(hipGetLastError());
+  return DEIG_OK;
+}
+
+int cheb_step_launch(const RRBuffers& b, float* T, int64_t d, int p, float thr, float alpha,
+                     float cc, float gamma, hipStream_t stream) {
+  DEIG_REQUIRE(p % 16 == 0, "cheb_step: p=%d must be a multiple of 16", p);
+  hipLaunchKernelGGL(cheb_step_kernel, dim3((unsigned)cdiv(d * (p / 4), 256)), dim3(256), 0,
+                     stream, b.Z, T, d, p, b.lam, thr, alpha, cc, gamma);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }

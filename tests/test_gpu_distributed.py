@@ -69,9 +69,12 @@ def test_world2_estimator_real_gpu_workers(tmp_path):
     assert r1["V"] is None and torch.equal(r0["Wt"], r1["Wt"])  # same gathered stack
     g = load_golden("spiked_d256_k10_m8")
     k = int(g["k"])
-    for i in range(world * wpr):  # rank-major, worker-minor == global shard order
-        Vi = r0["Wt"][i * k:(i + 1) * k].t().double().numpy()
-        assert ref_cpu.projector_distance(Vi, g["worker_V"][i]) <= P_TOL, i
+    # the golden worker bases are stored in the reference run's arrival (LIFO) order
+    by_range = {tuple(int(v) for v in r): i for i, r in enumerate(g["ranges"])}
+    shards = ref_cpu.split_batches(g["X"].shape[0], world * wpr)
+    for s, (lo, hi) in enumerate(shards):  # rank-major, worker-minor == global shard order
+        Vs = r0["Wt"][s * k:(s + 1) * k].t().double().numpy()
+        assert ref_cpu.projector_distance(Vs, g["worker_V"][by_range[(lo, hi)]]) <= P_TOL, s
     _, _, sw, sv = ref_cpu.one_shot(g["X"], k, int(g["m"]))
     assert ref_cpu.projector_distance(r0["V"].numpy(), sv) <= P_TOL
     np.testing.assert_allclose(r0["evals"].numpy(), sw, rtol=EV_TOL)
