@@ -558,7 +558,9 @@ __global__ __launch_bounds__(256) void cheb_step_kernel(float* __restrict__ Z,
   const f32x4 y = *reinterpret_cast<const f32x4*>(Z + r * 2 * p + p + j);
   f32x4* tp = reinterpret_cast<f32x4*>(T + r * p + j);
   const f32x4 q = *zq;
-  const f32x4 t = *tp;
+  // degree 1 (gamma == 0) must not read T: it is uninitialised workspace then
+  // (0 * NaN garbage would poison the column)
+  const f32x4 t = gamma != 0.f ? *tp : f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 xn = q;
 #pragma unroll
   for (int u = 0; u < 4; ++u)
