@@ -100,6 +100,7 @@ SolverWs carve_solver(void* ws, size_t cap, int64_t d, int k, int p, int64_t mk,
   w.rr.W = c.take<float>((size_t)p * p);
   w.rr.lam = c.take<float>((size_t)p);
   w.rr.cs = c.take<float>((size_t)p);
+  w.rr.qs = c.take<float>((size_t)p);
   w.rr.resid_part = c.take<float>((size_t)rr_update_blocks(d) * k);
   w.rr.resid = c.take<float>((size_t)k + 1);
   w.rr.info = c.take<int>(16);

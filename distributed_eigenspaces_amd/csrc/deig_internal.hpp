@@ -108,6 +108,7 @@ struct RRBuffers {
   float* W;          // p x p, columns sorted by descending Ritz value
   float* lam;        // p, descending
   float* cs;         // p, column scales (0 = dead column)
+  float* qs;         // p, 1 / ||Q w_j|| (Ritz vector normalisation)
   float* resid_part; // nblk_update x k
   float* resid;      // k  (relative residual per top-k column; [k] = max)
   int* info;         // small int scratch

@@ -104,6 +104,7 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
                                                       float* __restrict__ Wout,
                                                       float* __restrict__ lam_out,
                                                       float* __restrict__ cs_out,
+                                                      float* __restrict__ qs_out,
                                                       int* __restrict__ info, int max_jsweeps) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int pp = p * p;
@@ -116,7 +117,8 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
   // p/2 rotations {cos, sin, row a, row b} (16-byte aligned: p % 16 == 0)
   f32x4* rotp = reinterpret_cast<f32x4*>(gd + p);
   int* rank = reinterpret_cast<int*>(rotp + half);  // p
-  float* red = reinterpret_cast<float*>(rank + p);  // RT/64 + 2
+  float* nq = reinterpret_cast<float*>(rank + p);   // p: ||Q w_j||^2
+  float* red = nq + p;                              // RT/64 + 2
   int* nrot = reinterpret_cast<int*>(red + RT / 64 + 2);
   const int tid = threadIdx.x;
   const int ldc = 2 * p;
@@ -402,6 +404,34 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
     float s = 0.f;
     for (int a = 0; a < p; ++a) s += X1[a * p + j];
     gd[j] = s;
+  }
+  __syncthreads();
+  // ---- 9. n_j = w_j^T M w_j = ||Q w_j||^2: 1 up to rounding when D M D was
+  //         factored exactly, but not for columns whose pivot was floored (a
+  //         numerically dependent Q): their Ritz vectors are renormalised by it,
+  //         or repeated floored RR steps compound their norms until they overflow.
+  for (int idx = tid; idx < pp; idx += RT) {
+    const int a = idx / p, b = idx - a * p;
+    X1[idx] = Mg[a * ldc + b];
+  }
+  __syncthreads();
+  {
+    float acc[4][4];
+    int a0, b0;
+    const bool act = lds_gemm4(X1, X2, p, tid, acc, a0, b0);
+    __syncthreads();
+    if (act)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          X1[(a0 + r) * p + b0 + c] = acc[r][c] * X2[(a0 + r) * p + b0 + c];
+    __syncthreads();
+  }
+  for (int j = tid; j < p; j += RT) {
+    float s = 0.f;
+    for (int a = 0; a < p; ++a) s += X1[a * p + j];
+    nq[j] = s;
     const float lj = lamv[j];
     int rk = 0;
     for (int b = 0; b < p; ++b) {
@@ -422,6 +452,7 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
     const int rk = rank[j];
     lam_out[rk] = lamv[j];
     cs_out[rk] = (gd[j] > gthr && gd[j] > 0.f) ? rsqrtf(gd[j]) : 0.f;
+    qs_out[rk] = (nq[j] > 1e-30f && isfinite(nq[j])) ? rsqrtf(nq[j]) : 1.f;
   }
   for (int idx = tid; idx < pp; idx += RT) {
     const int a = idx / p, j = idx - a * p;
@@ -434,6 +465,7 @@ __global__ __launch_bounds__(256) void rr_update_kernel(float* __restrict__ Z, i
                                                         int k, const float* __restrict__ W,
                                                         const float* __restrict__ lam,
                                                         const float* __restrict__ cs,
+                                                        const float* __restrict__ qs,
                                                         float* __restrict__ V, int64_t ldv,
                                                         float* __restrict__ resid_part) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -453,7 +485,7 @@ __global__ __launch_bounds__(256) void rr_update_kernel(float* __restrict__ Z, i
   __syncthreads();
   const int grp = tid / p, j = tid - grp * p;
   if (grp < ngrp) {
-    const float lj = lam[j], cj = cs[j];
+    const float lj = lam[j], cj = cs[j], qj = qs[j];
     float racc = 0.f;
     for (int rr = grp; rr < UR; rr += ngrp) {
       const int64_t row = r0 + rr;
@@ -466,12 +498,14 @@ __global__ __launch_bounds__(256) void rr_update_kernel(float* __restrict__ Z, i
         qw = fmaf(zq[a], w, qw);
         yw = fmaf(zy[a], w, yw);
       }
+      qw *= qj;  // unit Ritz vector (qs = 1 / ||Q w_j||)
+      yw *= qj;
       if (j < k) {
         const float e = yw - lj * qw;
         racc = fmaf(e, e, racc);
         V[row + (int64_t)(k - 1 - j) * ldv] = qw;
       }
-      Z[row * ld + j] = (cj > 0.f) ? yw * cj : qw;
+      Z[row * ld + j] = (cj > 0.f) ? yw * (cj / qj) : qw;
     }
     if (j < k) rp[grp * k + j] = racc;
   }
@@ -570,7 +604,7 @@ __global__ __launch_bounds__(256) void cheb_step_kernel(float* __restrict__ Z,
 }
 
 size_t rr_small_shm(int p) {
-  return (size_t)(2 * p * p + 6 * p + RT / 64 + 20) * sizeof(float);
+  return (size_t)(2 * p * p + 7 * p + RT / 64 + 20) * sizeof(float);
 }
 
 }  // namespace
@@ -595,7 +629,7 @@ int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream, int max_jswee
     attr = true;
   }
   hipLaunchKernelGGL(rr_small_kernel, dim3(1), dim3(RT), shm, stream, b.C, p, b.W, b.lam, b.cs,
-                     b.info, max_jsweeps);
+                     b.qs, b.info, max_jsweeps);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }
@@ -631,7 +665,7 @@ int rr_update_launch(const RRBuffers& b, int64_t d, int p, int k, float* V, int6
     attr = true;
   }
   hipLaunchKernelGGL(rr_update_kernel, dim3(nblk), dim3(256), shm, stream, b.Z, d, p, k, b.W,
-                     b.lam, b.cs, V, ldv, b.resid_part);
+                     b.lam, b.cs, b.qs, V, ldv, b.resid_part);
   DEIG_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(rr_finish_kernel, dim3(1), dim3(256), 0, stream, b.resid_part, nblk, k, b.lam,
                      evals, b.resid);

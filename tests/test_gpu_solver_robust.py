@@ -107,3 +107,21 @@ def test_no_guard_columns_p_equals_k(cuda):
     w, V = ref_cpu.top_k_eigh(S.astype(np.float64), k)
     assert ref_cpu.projector_distance(r.V.cpu().numpy(), V) <= P_TOL
     np.testing.assert_allclose(r.evals.cpu().numpy(), w, rtol=EV_TOL)
+
+
+@pytest.mark.parametrize("d,k,m", [(256, 6, 2), (512, 10, 2), (1024, 16, 1), (300, 7, 3)])
+def test_projavg_rank_deficient_stack(d, k, m, cuda):
+    """Fewer stacked basis rows than subspace columns (m k < p): the operator is
+    rank-deficient, the RR Cholesky floors pivots on the null columns, and their
+    Ritz vectors must be renormalised (r02: their norms compounded to inf).
+    Against the float64 server solve (distributed.py:126-130 + NB:306)."""
+    import distributed_eigenspaces_amd as de
+    rng = np.random.default_rng(d + m)
+    U = np.linalg.qr(rng.standard_normal((d, k)))[0]
+    Vs = [np.linalg.qr(U + 0.05 * rng.standard_normal((d, k)))[0] for _ in range(m)]
+    Wt = de.stack_bases([torch.from_numpy(v).float().to(cuda) for v in Vs])
+    r = de.projavg_topk(Wt, k, 1.0 / m, q0=torch.from_numpy(Vs[0]).float().to(cuda))
+    assert r.converged
+    w, V = ref_cpu.server_topk([v.astype(np.float32).astype(np.float64) for v in Vs], k, m)
+    assert ref_cpu.projector_distance(r.V.cpu().numpy(), V) <= P_TOL
+    np.testing.assert_allclose(r.evals.cpu().numpy(), w, rtol=EV_TOL)
