@@ -176,15 +176,20 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
       sd = sum8(sd);
       so = sum8(so);
       float v = X1[j * p + j] - sd;
+      // A pivot below 1e-6 (the column's part independent of the earlier ones is
+      // < 1e-3 of its norm: numerically dependent) decouples the column: unit
+      // pivot, zero sub-diagonal.  Its orthogonalised vector is then the tiny
+      // Gram-Schmidt residual (Ritz value ~0, renormalised in rr_update by qs),
+      // and L^-1 stays bounded - dividing the sub-diagonal by a floored pivot
+      // grew L^-1 geometrically over consecutive dependent columns (r02: inf).
       const bool floored = !(v > 1e-6f);
-      if (floored) v = 1e-6f;
-      const float ljj = sqrtf(v);
+      const float ljj = floored ? 1.0f : sqrtf(v);
       if (part == 0) {
         if (i == j) {
           gd[j] = ljj;
           if (floored) info[0] += 1;
         } else {
-          X1[i * p + j] = (X1[i * p + j] - so) / ljj;
+          X1[i * p + j] = floored ? 0.f : (X1[i * p + j] - so) / ljj;
         }
       }
     }
