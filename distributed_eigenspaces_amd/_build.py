@@ -13,8 +13,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdeig.so")
-SOURCES = ["capi.hip", "syrk.hip", "syrk_split.hip", "skinny.hip", "rr.hip", "oja.hip", "project.hip",
-           "sweep.hip"]
+SOURCES = ["capi.hip", "syrk.hip", "syrk_split.hip", "syrk_u8.hip", "skinny.hip", "rr.hip", "oja.hip",
+           "project.hip", "sweep.hip"]
 # Per-source extra flags.  sweep.hip: keep the split's scalar f32 subtractions
 # unpacked (v_pk_add_f32 beside MFMAs costs issue cycles, MI355X_MICROARCH.md).
 EXTRA_FLAGS = {"sweep.hip": ["-fno-slp-vectorize"]}

@@ -30,6 +30,9 @@ DEIG_SWEEP_FP32 = 2
 DEIG_SWEEP_PREPARED = 0x100
 DEIG_SWEEP_ROUND_Q = 0x200
 SWEEP_ALGOS = {"auto": DEIG_SWEEP_AUTO, "bf16x6": DEIG_SWEEP_BF16X6, "fp32": DEIG_SWEEP_FP32}
+DEIG_U8_RAW = 0
+DEIG_U8_GRAY3 = 1
+U8_MODES = {"raw": DEIG_U8_RAW, "gray": DEIG_U8_GRAY3}
 
 _c_i64 = ctypes.c_int64
 _c_sz = ctypes.c_size_t
@@ -45,6 +48,9 @@ SIGNATURES = {
     "deig_syrk_f32_ex": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, ctypes.c_float, _fp,
                                         _c_i64, ctypes.c_int, _vp, _c_sz, _vp]),
     "deig_syrk_workspace_ex": (_c_sz, [_c_i64, _c_i64, ctypes.c_int]),
+    "deig_syrk_u8": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, ctypes.c_int, ctypes.c_double,
+                                    _fp, _c_i64, _fp, _c_i64, _vp, _c_sz, _vp]),
+    "deig_syrk_u8_workspace": (_c_sz, [_c_i64, _c_i64, ctypes.c_int]),
     "deig_default_subspace": (ctypes.c_int, [_c_i64, ctypes.c_int]),
     "deig_topk_sym_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_float, _fp, ctypes.c_int, _c_i64,

@@ -387,6 +387,18 @@ int deig_syrk_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha
   return deig_syrk_f32_ex(X, n, d, ldx, alpha, S, lds, DEIG_SYRK_DEFAULT, ws, ws_bytes, stream);
 }
 
+size_t deig_syrk_u8_workspace(int64_t n, int64_t d, int mode) {
+  return syrk_u8_workspace_bytes(n, d, mode);
+}
+
+int deig_syrk_u8(const uint8_t* X, int64_t n, int64_t d, int64_t ldx, int mode, double alpha,
+                 float* S, int64_t lds, double* S64, int64_t lds64, void* ws, size_t ws_bytes,
+                 void* stream) {
+  g_err[0] = 0;
+  return syrk_u8_launch(X, n, d, ldx, mode, alpha, S, lds, S64, lds64, ws, ws_bytes,
+                        (hipStream_t)stream);
+}
+
 int deig_default_subspace(int64_t d, int k) {
   int64_t p = ((int64_t)k + (k < 16 ? 8 : k / 4) + 15) / 16 * 16;
   if (p > kMaxP) p = kMaxP;

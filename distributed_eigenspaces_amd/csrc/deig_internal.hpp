@@ -73,6 +73,12 @@ size_t syrk_split_workspace_bytes(int64_t n, int64_t d);
 int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha, float* S,
                       int64_t lds, void* ws, size_t ws_bytes, hipStream_t stream);
 
+// Exact uint8 covariance on int8 MFMA (syrk_u8.hip); mode DEIG_U8_RAW / DEIG_U8_GRAY3.
+size_t syrk_u8_workspace_bytes(int64_t n, int64_t d, int mode);
+int syrk_u8_launch(const uint8_t* X, int64_t n, int64_t d, int64_t ldx, int mode, double alpha,
+                   float* S, int64_t lds, double* S64, int64_t lds64, void* ws, size_t ws_bytes,
+                   hipStream_t stream);
+
 // Skinny GEMM (skinny.hip):  C[M x N] = alpha * op(A) * B + beta * C
 //   trans_a = true : A is K x M row-major (op(A) = A^T)
 //   trans_a = false: A is M x K row-major

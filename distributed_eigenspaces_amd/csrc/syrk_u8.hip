@@ -1,0 +1,384 @@
+// Exact covariance of uint8 samples on CDNA4 int8 MFMA (fused
+// ingest):  S = alpha * V^T V  with V the n x d feature matrix of
+//   DEIG_U8_RAW  : v = x (one byte per feature, d bytes of each row);
+//   DEIG_U8_GRAY3: v = (r + g + b) / 3 for interleaved pixels (3 bytes per feature) -
+//                  the reference's grayscale + flatten, distributed.py:170-173
+//                  (data.mean(axis=3), reshape to 1024) followed by :59-70.
+// The reference computes in float64 from the uint8 CIFAR bytes (load_data.py:18-33);
+// here every product and sum is EXACT (integers), so S is the correctly rounded
+// fp32 (or fp64) value of the reference's result - no accumulation error at all,
+// which an fp32 SYRK of uncentered 0..255 data cannot offer (its rounding noise
+// ~5e-7 max|S| alone moves a CIFAR-like top-k basis by ~3e-4 in ||P - P_ref||_F).
+//
+// Integer decomposition (all operands int8, v_mfma_i32_16x16x64_i8, int32 acc):
+//   raw : y = x - 128 (= x ^ 0x80 as int8);
+//         sum x_i x_j = sum y_i y_j + 128 (Y_i + Y_j) + 128^2 n,   Y = column sums of y
+//   gray: s = r + g + b in [0, 765], t = s - 384 in [-384, 381] = 16 h + l,
+//         h = t >> 4 in [-24, 23], l = t & 15, w = h + l in [-24, 38]  (three planes);
+//         sum t_i t_j = 240 P_hh + 16 P_ww - 15 P_ll   (P_ww - P_hh - P_ll = the cross term)
+//         sum s_i s_j = sum t_i t_j + 384 (T_i + T_j) + 384^2 n,   T = column sums of t,
+//         and v = s / 3 gives the factor 1/9.
+// Pipeline: u8_prep_kernel (X -> int8 planes in MFMA operand order + int64 column
+// sums), u8_syrk_kernel (128 x 128 lower tiles x K segments x planes, LDS double
+// buffer, int32 MFMA accumulators, int64 atomic adds: exact and order independent,
+// hence deterministic), u8_finalize_kernel (combine planes + corrections in int64,
+// one double rounding, both triangles from the same value: bit-exact symmetry).
+#include "deig_internal.hpp"
+
+namespace deig {
+namespace {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int KB = 64;        // rows per K-step (one MFMA 16x16x64 depth)
+constexpr int TB = 128;       // output tile edge (features)
+constexpr int FPAD = 128;     // features padded to a multiple of this
+constexpr int SYRK_THR = 256;  // 4 waves, 2 x 2 wave tiles of 64 x 64
+constexpr int PREP_THR = 64;   // prep: one wave, 4 features per lane
+constexpr int MAX_SEG_KB = 1024;  // <= 65536 rows per item: int32 accumulators cannot overflow
+constexpr int PREP_YB = 128;
+
+inline int u8_planes(int mode) { return mode == DEIG_U8_GRAY3 ? 3 : 1; }
+
+// Image: plane-major, then [kb][g = 16-row group][feature][16 bytes = rows 16g..16g+15].
+__host__ __device__ inline int64_t img_off(int64_t plane, int64_t kb, int g, int64_t f, int64_t nkb,
+                                           int64_t fpad) {
+  return (((plane * nkb + kb) * 4 + g) * fpad + f) * 16;
+}
+
+// 4 x 4 byte transpose: r[q] holds byte u = feature u of row q; out[u] holds byte q =
+// row q of feature u.
+__device__ __forceinline__ void tr4(const uint32_t r[4], uint32_t out[4]) {
+  const uint32_t lo01 = __builtin_amdgcn_perm(r[1], r[0], 0x05010400u);
+  const uint32_t hi01 = __builtin_amdgcn_perm(r[1], r[0], 0x07030602u);
+  const uint32_t lo23 = __builtin_amdgcn_perm(r[3], r[2], 0x05010400u);
+  const uint32_t hi23 = __builtin_amdgcn_perm(r[3], r[2], 0x07030602u);
+  out[0] = __builtin_amdgcn_perm(lo23, lo01, 0x05040100u);
+  out[1] = __builtin_amdgcn_perm(lo23, lo01, 0x07060302u);
+  out[2] = __builtin_amdgcn_perm(hi23, hi01, 0x05040100u);
+  out[3] = __builtin_amdgcn_perm(hi23, hi01, 0x07060302u);
+}
+
+__device__ __forceinline__ int sbyte(uint32_t v, int u) { return (int)(int8_t)(v >> (8 * u)); }
+
+// grid (fpad / 256, YB): lane owns features f .. f + 3 (f = 256 bx + 4 lane) and
+// walks row blocks kb = by, by + YB, ...; per 16-row group it loads one dword
+// (raw) or three (gray) per row, forms the int8 plane values, transposes 4 x 4
+// byte blocks and writes 16 B per feature and plane (coalesced across lanes).
+template <int MODE>
+__global__ __launch_bounds__(PREP_THR) void u8_prep_kernel(const uint8_t* __restrict__ X,
+                                                           int64_t n, int64_t ldx, int d,
+                                                           int64_t fpad, int64_t nkb,
+                                                           uint8_t* __restrict__ img,
+                                                           unsigned long long* __restrict__ colsum) {
+  constexpr int NP = MODE == DEIG_U8_GRAY3 ? 3 : 1;
+  const int f = blockIdx.x * 256 + threadIdx.x * 4;
+  const bool fin = f < d;  // d % 4 == 0: the 4 features are all in or all out
+  int csum[4] = {0, 0, 0, 0};
+  for (int64_t kb = blockIdx.y; kb < nkb; kb += gridDim.y) {
+    for (int g = 0; g < 4; ++g) {
+      uint32_t rows[NP][16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = kb * KB + g * 16 + r;
+        const bool ok = fin && row < n;
+        if (MODE == DEIG_U8_RAW) {
+          const uint32_t x = ok ? *reinterpret_cast<const uint32_t*>(X + row * ldx + f) : 0x80808080u;
+          const uint32_t y = x ^ 0x80808080u;  // int8 (x - 128); padding rows -> 0
+          rows[0][r] = y;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) csum[u] += sbyte(y, u);
+        } else {
+          uint32_t b[3] = {0u, 0u, 0u};
+          if (ok) {
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(X + row * ldx + 3 * (int64_t)f);
+            b[0] = p[0];
+            b[1] = p[1];
+            b[2] = p[2];
+          }
+          uint32_t ph = 0, pl = 0, pw = 0;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            int s = 0;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              const int byte = 3 * u + c;
+              s += (int)((b[byte >> 2] >> (8 * (byte & 3))) & 0xffu);
+            }
+            const int t = ok ? s - 384 : 0;  // padding rows contribute nothing
+            const int h = t >> 4, l = t & 15, w = h + l;
+            csum[u] += t;
+            ph |= ((uint32_t)h & 0xffu) << (8 * u);
+            pl |= ((uint32_t)l & 0xffu) << (8 * u);
+            pw |= ((uint32_t)w & 0xffu) << (8 * u);
+          }
+          rows[0][r] = ph;
+          rows[NP > 1 ? 1 : 0][r] = pl;
+          rows[NP > 2 ? 2 : 0][r] = pw;
+        }
+      }
+      if (f >= fpad) continue;
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl) {
+        uint32_t col[4][4];  // [feature u][dword q]
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          uint32_t t4[4];
+          tr4(&rows[pl][4 * q], t4);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) col[u][q] = t4[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          *reinterpret_cast<u32x4*>(img + img_off(pl, kb, g, f + u, nkb, fpad)) =
+              u32x4{col[u][0], col[u][1], col[u][2], col[u][3]};
+      }
+    }
+  }
+  if (fin) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      atomicAdd(colsum + f + u, (unsigned long long)(long long)csum[u]);
+  }
+}
+
+struct U8Sched {
+  const uint8_t* img;
+  unsigned long long* G;  // planes x fpad x fpad int64 (two's complement), lower tiles
+  const int* order;       // lower tile list: ti | tj << 16
+  int64_t nkb, fpad;
+  int T, nseg;
+};
+
+// One item = (plane, lower tile, K segment).  LDS: 2 stages x (A panel, B panel),
+// each panel = 4 row groups x 128 features x 16 B = 8 KiB, the same bytes as the
+// image's [kb][g][f0 .. f0+127] runs.  Wave (wi, wj) owns rows 64 wi.. and columns
+// 64 wj.. of the tile: 4 x 4 MFMA blocks, lane l reads the A fragment of feature
+// 16 a + (l & 15), row group l >> 4 (16 consecutive rows = 16 bytes).
+__global__ __launch_bounds__(SYRK_THR) void u8_syrk_kernel(U8Sched s) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2][2][4 * TB * 16];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = tid >> 6, wi = wave >> 1, wj = wave & 1;
+  const int item = blockIdx.x;
+  const int plane = blockIdx.y;
+  const int tile = item % s.T, seg = item / s.T;
+  const int tt = s.order[tile];
+  const int ti = tt & 0xffff, tj = tt >> 16;
+  const bool diag = ti == tj;
+  const bool active = !(diag && wi < wj);  // the upper block of a diagonal tile is a mirror
+  const int64_t k0 = s.nkb * seg / s.nseg, k1 = s.nkb * (seg + 1) / s.nseg;
+  const int64_t i0 = (int64_t)ti * TB, j0 = (int64_t)tj * TB;
+
+  // staging: thread t moves 16 B chunks c = t and t + 256 of each panel (512 chunks
+  // = 4 groups x 128 features)
+  auto load = [&](int64_t kb, u32x4 (&ra)[2], u32x4 (&rb)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = tid + h * SYRK_THR;
+      const int g = c >> 7, fl = c & 127;
+      ra[h] = *reinterpret_cast<const u32x4*>(s.img + img_off(plane, kb, g, i0 + fl, s.nkb, s.fpad));
+      if (!diag)
+        rb[h] = *reinterpret_cast<const u32x4*>(s.img + img_off(plane, kb, g, j0 + fl, s.nkb, s.fpad));
+    }
+  };
+  auto put = [&](int st, const u32x4 (&ra)[2], const u32x4 (&rb)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = tid + h * SYRK_THR;
+      *reinterpret_cast<u32x4*>(&lds[st][0][c * 16]) = ra[h];
+      if (!diag) *reinterpret_cast<u32x4*>(&lds[st][1][c * 16]) = rb[h];
+    }
+  };
+
+  i32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = i32x4{0, 0, 0, 0};
+
+  u32x4 ra[2], rb[2];
+  if (k0 < k1) {
+    load(k0, ra, rb);
+    put(0, ra, rb);
+  }
+  __syncthreads();
+  int st = 0;
+  for (int64_t kb = k0; kb < k1; ++kb) {
+    const bool more = kb + 1 < k1;
+    if (more) load(kb + 1, ra, rb);  // in flight while this stage's MFMAs run
+    if (active) {
+      const uint8_t* pa = &lds[st][0][0];
+      const uint8_t* pb = diag ? pa : &lds[st][1][0];
+      const int g = lane >> 4, c = lane & 15;
+      i32x4 fa[4], fb[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        fa[a] = *reinterpret_cast<const i32x4*>(pa + (g * TB + 64 * wi + 16 * a + c) * 16);
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        fb[b] = *reinterpret_cast<const i32x4*>(pb + (g * TB + 64 * wj + 16 * b + c) * 16);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
+    }
+    if (more) put(st ^ 1, ra, rb);
+    __syncthreads();
+    st ^= 1;
+  }
+  if (!active || k0 >= k1) return;
+  // C/D map (gfx950, dtype independent): column = lane & 15, row = 4 (lane >> 4) + reg
+  unsigned long long* Gp = s.G + (int64_t)plane * s.fpad * s.fpad;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t i = i0 + 64 * wi + 16 * a + 4 * (lane >> 4) + r;
+        const int64_t j = j0 + 64 * wj + 16 * b + (lane & 15);
+        if (diag && j > i) continue;
+        atomicAdd(Gp + i * s.fpad + j, (unsigned long long)(long long)acc[a][b][r]);
+      }
+}
+
+// One thread per S entry: the lower-triangle value of (max(i,j), min(i,j)) from
+// the exact int64 sums, scaled once in double, stored to both triangles.
+template <int MODE>
+__global__ __launch_bounds__(256) void u8_finalize_kernel(const unsigned long long* __restrict__ G,
+                                                          const unsigned long long* __restrict__ colsum,
+                                                          int64_t fpad, int64_t d, int64_t n,
+                                                          double alpha, float* __restrict__ S,
+                                                          int64_t lds, double* __restrict__ S64,
+                                                          int64_t lds64) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= d * d) return;
+  const int64_t r = idx / d, c = idx - r * d;
+  const int64_t i = r > c ? r : c, j = r > c ? c : r;
+  const long long ci = (long long)colsum[i], cj = (long long)colsum[j];
+  long long a;
+  double v;
+  if (MODE == DEIG_U8_RAW) {
+    a = (long long)G[i * fpad + j] + 128ll * (ci + cj) + 16384ll * n;
+    v = alpha * (double)a;
+  } else {
+    const int64_t pl = fpad * fpad;
+    const long long phh = (long long)G[i * fpad + j];
+    const long long pll = (long long)G[pl + i * fpad + j];
+    const long long pww = (long long)G[2 * pl + i * fpad + j];
+    a = 240ll * phh + 16ll * pww - 15ll * pll + 384ll * (ci + cj) + 147456ll * n;
+    v = alpha * (double)a / 9.0;
+  }
+  if (S) S[r * lds + c] = (float)v;
+  if (S64) S64[r * lds64 + c] = v;
+}
+
+__global__ void u8_tile_order_kernel(int nt, int* order) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int idx = 0;
+  for (int ti = 0; ti < nt; ++ti)
+    for (int tj = 0; tj <= ti; ++tj) order[idx++] = ti | (tj << 16);
+}
+
+struct U8Layout {
+  int64_t fpad, nkb, nt, T;
+  int planes;
+  size_t off_order, off_col, off_G, off_img, total;
+};
+
+U8Layout u8_layout(int64_t n, int64_t d, int mode) {
+  U8Layout L;
+  L.planes = u8_planes(mode);
+  L.fpad = cdiv(d, FPAD) * FPAD;
+  L.nkb = cdiv(n, KB);
+  L.nt = L.fpad / TB;
+  L.T = L.nt * (L.nt + 1) / 2;
+  size_t off = 0;
+  L.off_order = off;
+  off = align_up(off + sizeof(int) * (size_t)L.T, 256);
+  L.off_col = off;
+  off = align_up(off + sizeof(unsigned long long) * (size_t)L.fpad, 256);
+  L.off_G = off;
+  off = align_up(off + sizeof(unsigned long long) * (size_t)L.planes * L.fpad * L.fpad, 256);
+  L.off_img = off;
+  off += (size_t)L.planes * L.nkb * KB * L.fpad;
+  L.total = off;
+  return L;
+}
+
+}  // namespace
+
+size_t syrk_u8_workspace_bytes(int64_t n, int64_t d, int mode) {
+  if (n < 1 || d < 1) return 0;
+  return u8_layout(n, d, mode).total;
+}
+
+int syrk_u8_launch(const uint8_t* X, int64_t n, int64_t d, int64_t ldx, int mode, double alpha,
+                   float* S, int64_t lds, double* S64, int64_t lds64, void* ws, size_t ws_bytes,
+                   hipStream_t stream) {
+  DEIG_REQUIRE(mode == DEIG_U8_RAW || mode == DEIG_U8_GRAY3, "syrk_u8: unknown mode %d", mode);
+  DEIG_REQUIRE(n >= 1, "syrk_u8: n must be >= 1 (got %lld)", (long long)n);
+  DEIG_REQUIRE(d >= 4 && d % 4 == 0 && d <= (1 << 15),
+               "syrk_u8: d must be a multiple of 4 in [4, 32768] (got %lld)", (long long)d);
+  const int64_t need = mode == DEIG_U8_RAW ? d : 3 * d;
+  DEIG_REQUIRE(ldx >= need && ldx % 4 == 0, "syrk_u8: ldx must be >= %lld bytes and a multiple of 4",
+               (long long)need);
+  DEIG_REQUIRE(X && (reinterpret_cast<uintptr_t>(X) & 3u) == 0, "syrk_u8: X must be 4-byte aligned");
+  DEIG_REQUIRE(S || S64, "syrk_u8: need S and/or S64");
+  DEIG_REQUIRE(!S || lds >= d, "syrk_u8: lds must be >= d");
+  DEIG_REQUIRE(!S64 || lds64 >= d, "syrk_u8: lds64 must be >= d");
+  DEIG_REQUIRE(n <= (int64_t(1) << 40), "syrk_u8: n too large");
+  const U8Layout L = u8_layout(n, d, mode);
+  if (!ws || ws_bytes < L.total)
+    return fail(DEIG_EWORKSPACE, "syrk_u8: workspace %zu bytes < required %zu", ws_bytes, L.total);
+  char* base = static_cast<char*>(ws);
+  int* order = reinterpret_cast<int*>(base + L.off_order);
+  unsigned long long* col = reinterpret_cast<unsigned long long*>(base + L.off_col);
+  unsigned long long* G = reinterpret_cast<unsigned long long*>(base + L.off_G);
+  uint8_t* img = reinterpret_cast<uint8_t*>(base + L.off_img);
+  DEIG_HIP_CHECK(hipMemsetAsync(col, 0, sizeof(unsigned long long) * L.fpad, stream));
+  DEIG_HIP_CHECK(hipMemsetAsync(G, 0, sizeof(unsigned long long) * L.planes * L.fpad * L.fpad, stream));
+  hipLaunchKernelGGL(u8_tile_order_kernel, dim3(1), dim3(64), 0, stream, (int)L.nt, order);
+  DEIG_HIP_CHECK(hipGetLastError());
+  const int yb = (int)(L.nkb < PREP_YB ? L.nkb : PREP_YB);
+  const dim3 pg((unsigned)(L.fpad / 256 + (L.fpad % 256 ? 1 : 0)), (unsigned)yb);
+  if (mode == DEIG_U8_RAW)
+    hipLaunchKernelGGL(u8_prep_kernel<DEIG_U8_RAW>, pg, dim3(PREP_THR), 0, stream, X, n, ldx,
+                       (int)d, L.fpad, L.nkb, img, col);
+  else
+    hipLaunchKernelGGL(u8_prep_kernel<DEIG_U8_GRAY3>, pg, dim3(PREP_THR), 0, stream, X, n, ldx,
+                       (int)d, L.fpad, L.nkb, img, col);
+  DEIG_HIP_CHECK(hipGetLastError());
+  // K segments: enough items to fill the chip twice over, each <= MAX_SEG_KB row
+  // blocks (int32 accumulators) and >= 4 (amortise the staging prologue).
+  const int G_ = num_cus();
+  int64_t nseg = cdiv(2 * G_, L.T * L.planes);
+  const int64_t min_seg = cdiv(L.nkb, MAX_SEG_KB);
+  if (nseg < min_seg) nseg = min_seg;
+  if (nseg > cdiv(L.nkb, 4)) nseg = cdiv(L.nkb, 4) > min_seg ? cdiv(L.nkb, 4) : min_seg;
+  if (nseg < 1) nseg = 1;
+  U8Sched s;
+  s.img = img;
+  s.G = G;
+  s.order = order;
+  s.nkb = L.nkb;
+  s.fpad = L.fpad;
+  s.T = (int)L.T;
+  s.nseg = (int)nseg;
+  hipLaunchKernelGGL(u8_syrk_kernel, dim3((unsigned)(L.T * nseg), (unsigned)L.planes),
+                     dim3(SYRK_THR), 0, stream, s);
+  DEIG_HIP_CHECK(hipGetLastError());
+  const dim3 fg((unsigned)cdiv(d * d, 256));
+  if (mode == DEIG_U8_RAW)
+    hipLaunchKernelGGL(u8_finalize_kernel<DEIG_U8_RAW>, fg, dim3(256), 0, stream, G, col, L.fpad, d,
+                       n, alpha, S, lds, S64, lds64);
+  else
+    hipLaunchKernelGGL(u8_finalize_kernel<DEIG_U8_GRAY3>, fg, dim3(256), 0, stream, G, col, L.fpad,
+                       d, n, alpha, S, lds, S64, lds64);
+  DEIG_HIP_CHECK(hipGetLastError());
+  return DEIG_OK;
+}
+
+}  // namespace deig

@@ -23,7 +23,7 @@ from . import _lib
 __all__ = [
     "sigma_hat", "topk_eigh", "projavg_topk", "oja_step", "default_subspace",
     "EigResult", "require_device_tensor", "project", "stack_bases", "gemm_skinny",
-    "oja_steps", "sym_apply",
+    "oja_steps", "sym_apply", "sigma_hat_u8",
 ]
 
 DEFAULT_TOL = 1e-6
@@ -110,6 +110,12 @@ def sigma_hat(x: torch.Tensor, alpha: float | None = None,
     accumulation, see include/deig.h), "fp32" (f32 MFMA fma chain) or "auto"
     (default: split3 for n >= 1024 rows, fp32 below).
     """
+    if not isinstance(x, torch.Tensor):
+        x = torch.as_tensor(x)
+    if x.dtype == torch.uint8:
+        # uint8 samples: the exact integer path (2-D raw bytes, or N x H x W x 3
+        # pixels with the reference's grayscale fused in)
+        return sigma_hat_u8(x, alpha=alpha, out=out)
     if algo not in _lib.SYRK_ALGOS:
         raise ValueError(f"algo must be one of {sorted(_lib.SYRK_ALGOS)}, got {algo!r}")
     code = _lib.SYRK_ALGOS[algo]
@@ -142,6 +148,76 @@ def sigma_hat(x: torch.Tensor, alpha: float | None = None,
         if out is not None:
             out.copy_(S)
             return out
+    return S
+
+
+def sigma_hat_u8(x: torch.Tensor, mode: str = "auto", alpha: float | None = None,
+                 out: torch.Tensor | None = None, dtype: torch.dtype = torch.float32) -> torch.Tensor:
+    """Exact Sigma_hat of uint8 samples on int8 MFMA (fused ingest).
+
+    x: uint8 tensor on the GPU (host arrays are copied over), either
+      * (n, d) raw bytes, mode "raw": V = x;
+      * (n, H, W, 3) interleaved pixels (CIFAR layout, load_data.py:18-33), mode
+        "gray": V = x.mean(axis=3).reshape(n, H*W) - the reference's preprocessing
+        distributed.py:170-173 - fused into the covariance; or (n, 3m) rows with
+        mode "gray" explicitly.
+    Returns alpha * V^T V (alpha = 1/n: distributed.py:59-70) as a (d, d) tensor of
+    ``dtype`` (float32: the correctly rounded value of the exact result; float64:
+    exact to double rounding).  Every product and sum is an integer computation
+    (include/deig.h deig_syrk_u8), so there is no accumulation error at all.
+    """
+    if not isinstance(x, torch.Tensor):
+        x = torch.as_tensor(x)
+    if x.dtype != torch.uint8:
+        raise ValueError(f"sigma_hat_u8 needs uint8 samples, got {x.dtype}")
+    if not torch.cuda.is_available():
+        raise RuntimeError("sigma_hat_u8: needs a ROCm GPU; there is no CPU fallback")
+    if x.device.type != "cuda":
+        x = x.to(torch.device("cuda", torch.cuda.current_device()))
+    if mode == "auto":
+        mode = "gray" if x.dim() == 4 else "raw"
+    if mode not in _lib.U8_MODES:
+        raise ValueError(f"mode must be 'auto', 'raw' or 'gray', got {mode!r}")
+    n = x.shape[0]
+    if mode == "gray":
+        if x.dim() == 4:
+            if x.shape[3] != 3:
+                raise ValueError(f"gray mode needs (n, H, W, 3) pixels, got {tuple(x.shape)}")
+            x = x.reshape(n, -1)
+        if x.dim() != 2 or x.shape[1] % 3:
+            raise ValueError("gray mode needs rows of 3-byte pixels")
+        d = x.shape[1] // 3
+    else:
+        if x.dim() != 2:
+            raise ValueError(f"raw mode needs a 2-D (n, d) tensor, got {tuple(x.shape)}")
+        d = x.shape[1]
+    if n == 0:
+        return torch.full((d, d), float("nan"), dtype=dtype, device=x.device)
+    a = (1.0 / n) if alpha is None else float(alpha)
+    width = 3 * d if mode == "gray" else d
+    dp = (d + 3) // 4 * 4
+    if x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 4 or dp != d:
+        wp = 3 * dp if mode == "gray" else dp
+        xx = torch.zeros((n, (wp + 3) // 4 * 4), dtype=torch.uint8, device=x.device)
+        xx[:, :width] = x[:, :width]
+        x = xx
+    if dtype not in (torch.float32, torch.float64):
+        raise ValueError("dtype must be torch.float32 or torch.float64")
+    S = torch.empty((dp, dp), dtype=dtype, device=x.device)
+    L = _lib.lib()
+    with torch.cuda.device(x.device):
+        nbytes = L.deig_syrk_u8_workspace(n, dp, _lib.U8_MODES[mode])
+        ws = _workspace(x.device, nbytes)
+        f32 = dtype == torch.float32
+        rc = L.deig_syrk_u8(x.data_ptr(), n, dp, x.stride(0), _lib.U8_MODES[mode], ctypes.c_double(a),
+                            S.data_ptr() if f32 else None, dp, None if f32 else S.data_ptr(), dp,
+                            ws.data_ptr(), nbytes, _stream(x.device))
+    _lib.check(rc, "deig_syrk_u8")
+    if dp != d:
+        S = S[:d, :d].contiguous()
+    if out is not None:
+        out.copy_(S)
+        return out
     return S
 
 

@@ -71,6 +71,26 @@ int deig_syrk_f32_ex(const float* X, int64_t n, int64_t d, int64_t ldx, float al
                      float* S, int64_t lds, int algo, void* ws, size_t ws_bytes, void* stream);
 size_t deig_syrk_workspace_ex(int64_t n, int64_t d, int algo);
 
+/* Exact covariance of uint8 samples (fused ingest):
+ *   S = alpha * V^T V,  V the n x d feature matrix of
+ *   DEIG_U8_RAW:   v = x, the first d bytes of each row (e.g. raw CIFAR rows, d = 3072);
+ *   DEIG_U8_GRAY3: v = (r + g + b) / 3 of d interleaved 3-byte pixels (row needs 3d
+ *                  bytes) - the reference's grayscale + flatten, distributed.py:170-173
+ *                  (data.mean(axis=3), reshape), fused into the covariance.
+ * Replaces compute_sigma_hat_ (distributed.py:59-70) on the uint8 CIFAR bytes of
+ * load_data.py:18-33 (alpha = 1/n reproduces the reference).  Every product and
+ * sum is exact (int8 MFMA with int32 accumulation, int64 combination), so S is the
+ * correctly rounded fp32 value (S64: the fp64 value, optional, may be NULL; S may be
+ * NULL when S64 is given) of the reference's float64 result; both triangles are
+ * written (bit-exact symmetry).  Requires d % 4 == 0, d <= 32768, ldx % 4 == 0 bytes,
+ * X 4-byte aligned.  Workspace: deig_syrk_u8_workspace(n, d, mode). */
+#define DEIG_U8_RAW 0
+#define DEIG_U8_GRAY3 1
+int deig_syrk_u8(const uint8_t* X, int64_t n, int64_t d, int64_t ldx, int mode, double alpha,
+                 float* S, int64_t lds, double* S64, int64_t lds64, void* ws, size_t ws_bytes,
+                 void* stream);
+size_t deig_syrk_u8_workspace(int64_t n, int64_t d, int mode);
+
 /* Subspace size the solvers use for a given k when the caller passes p <= 0. */
 int deig_default_subspace(int64_t d, int k);
 
