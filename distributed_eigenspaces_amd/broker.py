@@ -7,7 +7,8 @@ build).  This broker keeps the exact call pattern - ``queue_declare``,
 routing_key, body)``, ``basic_ack``, ``start_consuming`` - so SlaveNode /
 MasterNode run unchanged inside one process, single-threaded (one event loop
 drives every consumer) or with ``my_threading.Slave`` threads (each thread
-serves its own channel).  Queues are FIFO, bodies are the same JSON strings.
+serves its own channel; several SlaveNodes on the "slaves" queue compete for its
+messages like RabbitMQ workers).  Queues are FIFO, bodies are the same JSON strings.
 
 Brokers are addressed by the ``broker_host`` string the nodes are given;
 ``connect(host)`` returns a connection to the broker registered under that name
@@ -27,7 +28,7 @@ class InProcBroker:
     def __init__(self, name: str = "inproc"):
         self.name = name
         self.queues: dict[str, deque] = {}
-        self.consumers: dict[str, "Channel"] = {}   # queue -> consuming channel
+        self.consumers: dict[str, list] = {}        # queue -> consuming channels (competing)
         self.callbacks: dict[str, callable] = {}
         self.active: set[int] = set()               # id(channel) with a thread in start_consuming
         self.cv = threading.Condition()
@@ -56,14 +57,18 @@ class InProcBroker:
             return sum(len(v) for v in self.queues.values())
 
     def _pick(self, ch: "Channel"):
-        """Next (queue, channel) this loop may serve: its own queues, plus queues whose
-        consumer channel has no thread of its own in start_consuming."""
+        """Next (queue, channel) this loop may serve: queues ``ch`` consumes (several
+        channels may consume one queue: competing consumers, like RabbitMQ workers
+        sharing a work queue), plus queues none of whose consumers has a thread of
+        its own in start_consuming (one loop then drives them all)."""
         for q, dq in self.queues.items():
-            if not dq or q not in self.consumers:
+            owners = self.consumers.get(q)
+            if not dq or not owners:
                 continue
-            owner = self.consumers[q]
-            if owner is ch or id(owner) not in self.active:
-                return q, owner
+            if ch in owners:
+                return q, ch
+            if not any(id(o) in self.active for o in owners):
+                return q, owners[0]
         return None
 
     def _others_active(self, ch) -> bool:
@@ -89,7 +94,7 @@ class InProcBroker:
                     self.delivered.append((q, body))
                     self._tag += 1
                     tag = self._tag
-                    cb = self.callbacks[q]
+                    cb = owner._callbacks[q]
                 data = body.encode() if isinstance(body, str) else body
                 cb(owner, types.SimpleNamespace(delivery_tag=tag, routing_key=q), None, data)
                 with self.cv:
@@ -104,6 +109,7 @@ class Channel:
     def __init__(self, broker: InProcBroker):
         self.broker = broker
         self._stop = False
+        self._callbacks: dict[str, callable] = {}
 
     def queue_declare(self, queue: str):
         self.broker.declare(queue)
@@ -111,7 +117,10 @@ class Channel:
     def basic_consume(self, queue: str, on_message_callback):
         with self.broker.cv:
             self.broker.queues.setdefault(queue, deque())
-            self.broker.consumers[queue] = self
+            owners = self.broker.consumers.setdefault(queue, [])
+            if self not in owners:
+                owners.append(self)
+            self._callbacks[queue] = on_message_callback
             self.broker.callbacks[queue] = on_message_callback
 
     def basic_publish(self, exchange: str = "", routing_key: str = "", body=""):

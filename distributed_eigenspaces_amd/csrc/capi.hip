@@ -59,6 +59,11 @@ constexpr int kMaxP = 128;
 constexpr float kStallAcceptTol = 4.0f;
 constexpr float kStallAcceptAbs = 2e-6f;
 constexpr int kStallGiveUp = 12;
+// Deflation stage of the explicit-matrix solver (see solve()): eigenpairs with
+// theta_j >= kDeflateRatio * theta_{k-1} (at most kMaxDeflate of them) are
+// deflated out of the sweep image and the rest iterated again.
+constexpr float kDeflateRatio = 64.f;
+constexpr int kMaxDeflate = 8;
 
 struct Operator {
   bool implicit;
@@ -234,10 +239,7 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
       (rc = sweep_prepare(op.S, d, op.lds, p, w.sweep_ws, w.sweep_bytes, st)))
     return rc;
   float lam_h[kMaxP];
-  float best = 3.4e38f;
-  int since_best = 0;
-  int it = 0;  // sweeps done
-  int nrr = 0;
+  int it = 0;  // sweeps done (both stages)
   float last = 3.4e38f;
   bool converged = false;
   // Sweeps round Q to two bf16 pieces (five products instead of six, sweep.hip
@@ -251,89 +253,136 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
       getenv("DEIG_JACOBI_EARLY_ABOVE") ? (float)atof(getenv("DEIG_JACOBI_EARLY_ABOVE")) : 1e-2f;
   static const float round_until =
       getenv("DEIG_SWEEP_ROUND_UNTIL") ? (float)atof(getenv("DEIG_SWEEP_ROUND_UNTIL")) : 1e-4f;
-  while (it < max_sweeps) {
-    const bool round_q = last > fmaxf(round_until, tol);
-    ChebPlan plan;
-    const bool cheb = cheb_on && nrr > 0 && cheb_plan(lam_h, k, p, last, tol, &plan);
-    int ncheb = 0;
-    if (cheb) {
-      // degree j: apply A to X_j, then X_{j+1} from X_j, A X_j and X_{j-1}
-      const int m = std::min(plan.m, max_sweeps - it - 1);
-      double s_prev = plan.s1;
-      for (int j = 0; j < m; ++j, ++it) {
-        if ((rc = apply_op(op, w, d, p, st, round_q))) return rc;
-        double alpha, gamma;
-        if (j == 0) {
-          alpha = plan.s1 / plan.e;
-          gamma = 0.0;
-        } else {
-          const double s_next = 1.0 / (2.0 / plan.s1 - s_prev);
-          alpha = 2.0 * s_next / plan.e;
-          gamma = s_prev * s_next;
-          s_prev = s_next;
+
+  // One stage of the iteration for the top kc pairs (V / evals columns 0..kc-1).
+  // Returns a status; sets converged / last; advances it.
+  auto iterate = [&](int kc) -> int {
+    float best = 3.4e38f;
+    int since_best = 0;
+    int nrr = 0;
+    last = 3.4e38f;
+    converged = false;
+    while (it < max_sweeps) {
+      const bool round_q = last > fmaxf(round_until, tol);
+      ChebPlan plan;
+      const bool cheb = cheb_on && nrr > 0 && cheb_plan(lam_h, kc, p, last, tol, &plan);
+      int ncheb = 0, rc2;
+      if (cheb) {
+        // degree j: apply A to X_j, then X_{j+1} from X_j, A X_j and X_{j-1}
+        const int m = std::min(plan.m, max_sweeps - it - 1);
+        double s_prev = plan.s1;
+        for (int j = 0; j < m; ++j, ++it) {
+          if ((rc2 = apply_op(op, w, d, p, st, round_q))) return rc2;
+          double alpha, gamma;
+          if (j == 0) {
+            alpha = plan.s1 / plan.e;
+            gamma = 0.0;
+          } else {
+            const double s_next = 1.0 / (2.0 / plan.s1 - s_prev);
+            alpha = 2.0 * s_next / plan.e;
+            gamma = s_prev * s_next;
+            s_prev = s_next;
+          }
+          if ((rc2 = cheb_step_launch(w.rr, w.T, d, p, plan.thr, (float)alpha, (float)plan.cc,
+                                      (float)gamma, st)))
+            return rc2;
         }
-        if ((rc = cheb_step_launch(w.rr, w.T, d, p, plan.thr, (float)alpha, (float)plan.cc,
-                                   (float)gamma, st)))
-          return rc;
+        ncheb = m;
+      } else if (nrr > 0) {
+        const int npow = std::min(rr_every - 1, max_sweeps - it - 1);
+        for (int j = 0; j < npow; ++j, ++it) {
+          if ((rc2 = apply_op(op, w, d, p, st, round_q))) return rc2;
+          // power step on the live Ritz columns of the last RR (Q_j <- Y_j / ||Y w_j||)
+          if ((rc2 = rr_power_launch(w.rr, d, p, tau, st))) return rc2;
+        }
       }
-      ncheb = m;
-    } else if (nrr > 0) {
-      const int npow = std::min(rr_every - 1, max_sweeps - it - 1);
-      for (int j = 0; j < npow; ++j, ++it) {
-        if ((rc = apply_op(op, w, d, p, st, round_q))) return rc;
-        // power step on the live Ritz columns of the last RR (Q_j <- Y_j / ||Y w_j||)
-        if ((rc = rr_power_launch(w.rr, d, p, tau, st))) return rc;
+      if ((rc2 = apply_op(op, w, d, p, st, round_q))) return rc2;
+      ++it;
+      if ((rc2 = skinny_launch(true, w.rr.Z, 2 * p, w.rr.Z, 2 * p, w.rr.C, 2 * p, 2 * p, 2 * p,
+                               d, 1.f, 0.f, w.slab, w.slab_bytes, st)))
+        return rc2;
+      // Early Rayleigh-Ritz steps (residual above jcap_above) run a capped number
+      // of Jacobi sweeps: the next basis Y W spans span(Y) for any invertible W, so
+      // subspace progress does not need converged Ritz vectors there; the residual
+      // of approximate pairs only over-states the error (no false convergence).
+      const int jcap = (jcap_sweeps > 0 && last > jcap_above) ? jcap_sweeps : 30;
+      if ((rc2 = rr_small_launch(w.rr, p, st, jcap))) return rc2;
+      if ((rc2 = rr_update_launch(w.rr, d, p, kc, V, ldv, evals, st))) return rc2;
+      DEIG_HIP_CHECK(
+          hipMemcpyAsync(&last, w.rr.resid + kc, sizeof(float), hipMemcpyDeviceToHost, st));
+      DEIG_HIP_CHECK(hipMemcpyAsync(lam_h, w.rr.lam, sizeof(float) * p, hipMemcpyDeviceToHost, st));
+      DEIG_HIP_CHECK(hipStreamSynchronize(st));
+      ++nrr;
+      if (debug) {
+        int inf[9] = {0};
+        DEIG_HIP_CHECK(hipMemcpy(inf, w.rr.info, sizeof(inf), hipMemcpyDeviceToHost));
+        fprintf(stderr, "[deig] d=%lld k=%d p=%d sweep %d resid %.3e cheb_deg %d chol_floor %d "
+                "jacobi_sweeps %d rotations %d small-solve us: chol %.1f linv %.1f congr %.1f "
+                "jacobi %.1f tail %.1f\n",
+                (long long)d, kc, p, it, last, ncheb, inf[0], inf[1], inf[2], inf[4] * 0.01,
+                (inf[5] - inf[4]) * 0.01, (inf[6] - inf[5]) * 0.01, (inf[7] - inf[6]) * 0.01,
+                (inf[8] - inf[7]) * 0.01);
+      }
+      if (!(last == last) || last > 3.0e38f)  // NaN / Inf
+        return fail(DEIG_EINVAL, "solver: non-finite residual (input contains NaN/Inf?)");
+      if (last <= tol) {
+        converged = true;
+        return DEIG_OK;
+      }
+      // Stagnation: no 10% improvement over the best residual for 4 Rayleigh-Ritz
+      // steps in a row.  It counts as convergence only at the fp32 floor (residual
+      // within kStallAccept* of tol); a stall above it is slow convergence (a small
+      // eigengap at k), so the iteration goes on and, if it stays stuck for
+      // kStallGiveUp RR steps, stops early with DEIG_NOT_CONVERGED.
+      if (last < 0.9f * best) {
+        best = last;
+        since_best = 0;
+      } else if (++since_best >= 4 && it >= 8) {
+        if (last <= fmaxf(kStallAcceptTol * tol, kStallAcceptAbs)) {
+          converged = true;
+          return DEIG_OK;
+        }
+        if (since_best >= kStallGiveUp) return DEIG_OK;
       }
     }
-    if ((rc = apply_op(op, w, d, p, st, round_q))) return rc;
-    ++it;
-    if ((rc = skinny_launch(true, w.rr.Z, 2 * p, w.rr.Z, 2 * p, w.rr.C, 2 * p, 2 * p, 2 * p, d,
-                            1.f, 0.f, w.slab, w.slab_bytes, st)))
+    return DEIG_OK;
+  };
+
+  rc = iterate(k);
+  if (rc) {
+    if (sweeps_out) *sweeps_out = it;
+    if (resid_out) *resid_out = last;
+    return rc;
+  }
+  // Stage 2 - deflation of dominant eigenpairs.  With theta_0 >> theta_{k-1} (an
+  // uncentered covariance: the mean direction dwarfs the rest, as for the
+  // reference's CIFAR bytes) every fp32 product S q loses ~log2(theta_0 / theta_k)
+  // bits of the small eigenvalues' directions to cancellation, which caps their
+  // accuracy far above the residual test's reach (relative to theta_0).  The r
+  // leading pairs with theta_j >= kDeflateRatio theta_{k-1} are then accurate
+  // (huge gap), so the sweep image is rebuilt as S - V_D Lam_D V_D^T and the
+  // remaining k - r pairs are iterated again from their current values (warm
+  // start), with the residual now relative to theta_r.  V_D stays in the last r
+  // columns of V (ascending order), which the second stage does not touch.
+  static const bool deflate_on = !(getenv("DEIG_DEFLATE") && getenv("DEIG_DEFLATE")[0] == '0');
+  if (deflate_on && converged && !op.implicit && w.sweep_ws && sweep_version() != 1 && k >= 2 &&
+      lam_h[k - 1] > 0.f && lam_h[0] >= kDeflateRatio * lam_h[k - 1]) {
+    int r = 0;
+    while (r < k - 1 && r < kMaxDeflate && lam_h[r] >= kDeflateRatio * lam_h[k - 1]) ++r;
+    const int kc = k - r;
+    const float* Vd = V + (int64_t)kc * ldv;
+    if ((rc = sweep_prepare(op.S, d, op.lds, p, w.sweep_ws, w.sweep_bytes, st, Vd, ldv,
+                            evals + kc, r)))
       return rc;
-    // Early Rayleigh-Ritz steps (residual above jcap_above) run a capped number
-    // of Jacobi sweeps: the next basis Y W spans span(Y) for any invertible W, so
-    // subspace progress does not need converged Ritz vectors there; the residual
-    // of approximate pairs only over-states the error (no false convergence).
-    const int jcap = (jcap_sweeps > 0 && last > jcap_above) ? jcap_sweeps : 30;
-    if ((rc = rr_small_launch(w.rr, p, st, jcap))) return rc;
-    if ((rc = rr_update_launch(w.rr, d, p, k, V, ldv, evals, st))) return rc;
-    DEIG_HIP_CHECK(hipMemcpyAsync(&last, w.rr.resid + k, sizeof(float), hipMemcpyDeviceToHost, st));
-    DEIG_HIP_CHECK(hipMemcpyAsync(lam_h, w.rr.lam, sizeof(float) * p, hipMemcpyDeviceToHost, st));
-    DEIG_HIP_CHECK(hipStreamSynchronize(st));
-    ++nrr;
-    if (debug) {
-      int inf[9] = {0};
-      DEIG_HIP_CHECK(hipMemcpy(inf, w.rr.info, sizeof(inf), hipMemcpyDeviceToHost));
-      fprintf(stderr, "[deig] d=%lld k=%d p=%d sweep %d resid %.3e cheb_deg %d chol_floor %d "
-              "jacobi_sweeps %d rotations %d small-solve us: chol %.1f linv %.1f congr %.1f "
-              "jacobi %.1f tail %.1f\n",
-              (long long)d, k, p, it, last, ncheb, inf[0], inf[1], inf[2], inf[4] * 0.01,
-              (inf[5] - inf[4]) * 0.01, (inf[6] - inf[5]) * 0.01, (inf[7] - inf[6]) * 0.01,
-              (inf[8] - inf[7]) * 0.01);
-    }
-    if (!(last == last) || last > 3.0e38f) {  // NaN / Inf
+    if ((rc = rr_init_launch(w.rr.Z, d, p, V, kc, ldv, 0x5eed5eefull, st))) return rc;
+    rc = iterate(kc);
+    if (debug)
+      fprintf(stderr, "[deig] deflated %d dominant pair(s): stage 2 resid %.3e after %d sweeps\n",
+              r, last, it);
+    if (rc) {
       if (sweeps_out) *sweeps_out = it;
       if (resid_out) *resid_out = last;
-      return fail(DEIG_EINVAL, "solver: non-finite residual (input contains NaN/Inf?)");
-    }
-    if (last <= tol) {
-      converged = true;
-      break;
-    }
-    // Stagnation: no 10% improvement over the best residual for 4 Rayleigh-Ritz
-    // steps in a row.  It counts as convergence only at the fp32 floor (residual
-    // within kStallAccept* of tol); a stall above it is slow convergence (a small
-    // eigengap at k), so the iteration goes on and, if it stays stuck for
-    // kStallGiveUp RR steps, stops early with DEIG_NOT_CONVERGED.
-    if (last < 0.9f * best) {
-      best = last;
-      since_best = 0;
-    } else if (++since_best >= 4 && it >= 8) {
-      if (last <= fmaxf(kStallAcceptTol * tol, kStallAcceptAbs)) {
-        converged = true;
-        break;
-      }
-      if (since_best >= kStallGiveUp) break;
+      return rc;
     }
   }
   if (sweeps_out) *sweeps_out = it;

@@ -96,8 +96,12 @@ int sweep_launch(const float* S, int64_t d, int64_t lds, const float* Q, int p, 
 // The same in two parts: sweep_prepare builds the S image in the workspace (once
 // per S), sweep_apply runs one product from it (S is still passed: the v1 kernel
 // reads it in place).
+// Vd / ldv / lamd / r (optional): the image is of S - Vd diag(lamd) Vd^T (r columns).
 int sweep_prepare(const float* S, int64_t d, int64_t lds, int p, void* ws, size_t ws_bytes,
-                  hipStream_t st);
+                  hipStream_t st, const float* Vd = nullptr, int64_t ldv = 0,
+                  const float* lamd = nullptr, int r = 0);
+// 1 = the row-major v1 sweep (reads S in place, no image, no deflation).
+int sweep_version();
 // round_q: the solver's in-place mode - Q (which must then be writable) is
 // rounded to 16 significant bits (Q' = h + m, two bf16 pieces) and the product
 // S Q' formed with five bf16 products instead of six (sweep.hip split_q_kernel).

@@ -322,10 +322,19 @@ size_t si_bytes(int64_t d) { return (size_t)si_rows(d) * si_groups(d) * 32 * 4; 
 // One thread per (rb, g, mb, lane): reads 32 contiguous bytes of one row, writes
 // the two 16-B halves (h = 0, 1) 1 KiB apart (d = 8192: 88 us = 6.1 TB/s of
 // read + write; an LDS-transposed variant with whole-row reads took 131 us).
+// Optional deflation (the eigensolver's second stage, capi.hip): the image is of
+// S - V_D diag(lam_D) V_D^T for r dominant eigenpairs (V_D column-major, ldv),
+// formed in fp32 with one fma per pair and element: the deflated entries then carry
+// about the rounding error of S itself, so products with the image no longer lose
+// the small eigenvalues' digits to cancellation against the dominant ones.
 __global__ __launch_bounds__(256) void sweep_prepare_kernel(const float* __restrict__ S,
                                                             int64_t lds, int64_t d, int64_t ng,
                                                             int64_t nunits,
-                                                            f32x4* __restrict__ SI) {
+                                                            f32x4* __restrict__ SI,
+                                                            const float* __restrict__ Vd,
+                                                            int64_t ldv,
+                                                            const float* __restrict__ lamd,
+                                                            int r) {
   const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (u >= nunits) return;
   const int lane = (int)(u & 63);
@@ -345,6 +354,15 @@ __global__ __launch_bounds__(256) void sweep_prepare_kernel(const float* __restr
       for (int e = 0; e < 4; ++e) {
         if (k + e < d) v0[e] = src[e];
         if (k + 4 + e < d) v1[e] = src[4 + e];
+      }
+    }
+    for (int q = 0; q < r; ++q) {
+      const float* vq = Vd + (int64_t)q * ldv;
+      const float a = -lamd[q] * vq[row];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (k + e < d) v0[e] = fmaf(a, vq[k + e], v0[e]);
+        if (k + 4 + e < d) v1[e] = fmaf(a, vq[k + 4 + e], v1[e]);
       }
     }
   }
@@ -673,6 +691,8 @@ size_t qs_bytes(int64_t d, int p) { return (size_t)cdiv(d, SW_KS) * SW_KS * p * 
 // rings spill), 2 (S image, independent waves with Q in registers), 3 (S image,
 // LDS-shared Q ring) or 1 (row-major S, register-staged Q stage, 8 waves);
 // DEIG_SWEEP_KERNEL selects one, for A/B timing.
+}  // namespace
+
 int sweep_version() {
   static int v = -1;
   if (v < 0) {
@@ -681,6 +701,8 @@ int sweep_version() {
   }
   return v;
 }
+
+namespace {
 
 template <int NB>
 void launch_v1(dim3 grid, hipStream_t st, const float* S, int64_t lds, int64_t d, const u32x4* QS,
@@ -773,7 +795,9 @@ SweepWs sweep_carve(void* ws, int64_t d, int p) {
 size_t sweep_workspace_bytes(int64_t d, int p) { return sweep_carve(nullptr, d, p).total; }
 
 int sweep_prepare(const float* S, int64_t d, int64_t lds, int p, void* ws, size_t ws_bytes,
-                  hipStream_t st) {
+                  hipStream_t st, const float* Vd, int64_t ldv, const float* lamd, int r) {
+  DEIG_REQUIRE(r == 0 || (Vd && lamd && ldv >= d && sweep_version() != 1),
+               "sweep: bad deflation arguments (r=%d)", r);
   DEIG_REQUIRE(d >= 1 && lds >= d && lds % 4 == 0 && S && aligned16(S),
                "sweep: S must be 16-byte aligned with lds >= d, lds %% 4 == 0");
   const SweepWs w = sweep_carve(ws, d, p);
@@ -783,7 +807,7 @@ int sweep_prepare(const float* S, int64_t d, int64_t lds, int p, void* ws, size_
   const int64_t ng = si_groups(d);
   const int64_t nunits = si_rows(d) / SI_RB * ng * 4 * 64;
   hipLaunchKernelGGL(sweep_prepare_kernel, dim3((unsigned)cdiv(nunits, 256)), dim3(256), 0, st, S,
-                     lds, d, ng, nunits, w.SI);
+                     lds, d, ng, nunits, w.SI, Vd, ldv, lamd, r);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }

@@ -29,7 +29,9 @@ from __future__ import annotations
 
 import argparse
 import json
+import threading
 import time
+from contextlib import nullcontext
 
 import numpy as np
 import torch
@@ -45,6 +47,31 @@ WINDOW = 5  # requests in flight at start (distributed.py:108)
 
 def _is_numpy(x) -> bool:
     return isinstance(x, np.ndarray) or not isinstance(x, torch.Tensor)
+
+
+_dev_cache: dict = {}
+_dev_lock = threading.Lock()
+
+
+def _device_copy(data) -> torch.Tensor:
+    """The node's data on the GPU, shared by every node given the same host array
+    (threaded workers hold one device copy).  uint8 samples stay uint8 (the exact
+    integer covariance path); everything else becomes float32."""
+    if isinstance(data, torch.Tensor) and data.is_cuda and data.dtype in (torch.uint8, torch.float32):
+        return data
+    with _dev_lock:
+        hit = _dev_cache.get(id(data))
+        if hit is not None and hit[0] is data:
+            return hit[1]
+        t = torch.as_tensor(data)
+        if t.dtype == torch.uint8:
+            if not torch.cuda.is_available():
+                raise RuntimeError("SlaveNode: needs a ROCm GPU; there is no CPU fallback")
+            dev = t.to(torch.device("cuda", torch.cuda.current_device()))
+        else:
+            dev = linalg.require_device_tensor(t, "SlaveNode.data")
+        _dev_cache[id(data)] = (data, dev)
+        return dev
 
 
 def top_k_eigh(matrix, k: int):
@@ -92,6 +119,7 @@ class SlaveNode(Node):
         print("Slave Start listening")
         self.data = data
         self._dev = None
+        self._stream = None
         self.channel.basic_consume(queue="slaves", on_message_callback=self.callback_)
 
     def start(self):
@@ -99,19 +127,23 @@ class SlaveNode(Node):
 
     def _device_data(self):
         if self._dev is None:
-            self._dev = linalg.require_device_tensor(self.data, "SlaveNode.data")
+            self._dev = _device_copy(self.data)
         return self._dev
 
     def callback_(self, channel, method, properties, body):
         request = json.loads(body)
         print("Slave: Received, batchid: " + str(request["batch"]))
         lo, hi = request["batch"][0], request["batch"][1]
-        batch = self._device_data()[lo:hi]
-        eigenspace = self.compute_sigma_hat_(batch)
-        eigenspace = self.top_k_eigenvectors(eigenspace, request["rank"])
-        response = dict()
-        response["batch"] = request["batch"]
-        response["eigenspace"] = eigenspace.double().cpu().numpy().tolist()
+        data = self._device_data()
+        if self._stream is None and data.is_cuda:  # one HIP stream per node: threaded nodes overlap
+            self._stream = torch.cuda.Stream(data.device)
+        with (torch.cuda.stream(self._stream) if self._stream is not None else nullcontext()):
+            batch = data[lo:hi]
+            eigenspace = self.compute_sigma_hat_(batch)
+            eigenspace = self.top_k_eigenvectors(eigenspace, request["rank"])
+            response = dict()
+            response["batch"] = request["batch"]
+            response["eigenspace"] = eigenspace.double().cpu().numpy().tolist()
         self.send_to_master_(str(json.dumps(response)))
         channel.basic_ack(delivery_tag=method.delivery_tag)
 

@@ -55,14 +55,15 @@ def test_extremes_and_long_shard(cuda):
     X[:, 1] = 0
     X[::2, 2] = 255
     S = de.linalg.sigma_hat_u8(torch.from_numpy(X).to(cuda), dtype=torch.float64)
-    ref = (X.astype(np.int64).T @ X.astype(np.int64)).astype(np.float64) / n
+    Xf = X.astype(np.float64)  # integer products and sums < 2^53: exact in float64
+    ref = (Xf.T @ Xf) / n
     np.testing.assert_allclose(S.cpu().numpy(), ref, rtol=1e-15, atol=0)
     img = rng.integers(0, 256, (70_000, 4, 4, 3), dtype=np.uint8)
     img[:, 0, 0, :] = 255
     img[:, 0, 1, :] = 0
     S = de.linalg.sigma_hat_u8(torch.from_numpy(img).to(cuda), dtype=torch.float64)
-    s = img.astype(np.int64).sum(axis=3).reshape(len(img), -1)
-    ref = (s.T @ s).astype(np.float64) / (9.0 * len(img))
+    s = img.astype(np.float64).sum(axis=3).reshape(len(img), -1)
+    ref = (s.T @ s) / (9.0 * len(img))
     np.testing.assert_allclose(S.cpu().numpy(), ref, rtol=1e-15, atol=0)
 
 
@@ -73,7 +74,8 @@ def test_strided_rows_and_alpha(cuda):
     W = rng.integers(0, 256, (3000, 1040), dtype=np.uint8)
     Xt = torch.from_numpy(W).to(cuda)[:, :1024]
     S = de.linalg.sigma_hat_u8(Xt, alpha=1.0, dtype=torch.float64)
-    ref = (W[:, :1024].astype(np.int64).T @ W[:, :1024].astype(np.int64)).astype(np.float64)
+    Wf = W[:, :1024].astype(np.float64)
+    ref = Wf.T @ Wf
     np.testing.assert_array_equal(S.cpu().numpy(), ref)
 
 

@@ -132,3 +132,30 @@ def test_connect_by_name_shares_broker():
     a = br.connect("shared-x").broker
     c = br.connect("shared-x").broker
     assert a is c
+
+
+def test_competing_slave_threads():
+    """Several SlaveNodes, each in its own my_threading.Slave thread on the same
+    "slaves" queue (RabbitMQ work-queue semantics: competing consumers): every shard
+    is computed exactly once and the master completes (config 1's 8 threaded
+    workers, distributed.py:33-57 + my_threading.py:6-15)."""
+    data = _data(n=4000, d=8)
+    m, nslaves = 13, 4
+    b = br.InProcBroker("t-compete")
+    slaves = [FakeSlave(b, data) for _ in range(nslaves)]
+    threads = [Slave(s.start) for s in slaves]
+    for t in threads:
+        t.start()
+    master = FakeMaster(b, 3, m, data)
+    master.start()
+    b.shutdown()
+    for t in threads:
+        t.join(raise_error=True)
+    assert len(master.batches_in_process) == 0
+    resps = [json.loads(body) for q, body in b.delivered if q == "master"]
+    step = data.shape[0] // m
+    assert sorted(tuple(r["batch"]) for r in resps) == [(i * step, (i + 1) * step) for i in range(m)]
+    for r in resps:
+        lo, hi = r["batch"]
+        V = np.array(r["eigenspace"])
+        assert V[0, 0] == hi - lo and V[1, 0] == data[lo, 0]
