@@ -376,6 +376,7 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
       return rc;
     if ((rc = rr_init_launch(w.rr.Z, d, p, V, kc, ldv, 0x5eed5eefull, st))) return rc;
     rc = iterate(kc);
+    if (!rc) rc = deflate_orth_launch(V, ldv, d, kc, r, st);
     if (debug)
       fprintf(stderr, "[deig] deflated %d dominant pair(s): stage 2 resid %.3e after %d sweeps\n",
               r, last, it);

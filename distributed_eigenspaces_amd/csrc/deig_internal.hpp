@@ -134,6 +134,8 @@ int cheb_step_launch(const RRBuffers& b, float* T, int64_t d, int p, float thr, 
                      float cc, float gamma, hipStream_t stream);
 int rr_update_launch(const RRBuffers& b, int64_t d, int p, int k, float* V, int64_t ldv,
                      float* evals, hipStream_t stream);
+// Columns 0..kc-1 of V (col-major, ldv) made orthogonal to columns kc..kc+r-1, normalised.
+int deflate_orth_launch(float* V, int64_t ldv, int64_t d, int kc, int r, hipStream_t stream);
 
 // Oja (oja.hip).
 size_t oja_workspace_bytes(int64_t b, int64_t d, int k);

@@ -608,6 +608,52 @@ __global__ __launch_bounds__(256) void cheb_step_kernel(float* __restrict__ Z,
   *zq = xn;
 }
 
+// After the deflated stage (capi.hip): V_j <- normalize(V_j - V_D V_D^T V_j) for the kc
+// stage-2 columns against the r deflated ones (V_D = columns kc .. kc + r - 1).  The
+// deflated operator S - lam_1 v^ v^T keeps a coupling lam_1 (v_1 d^T + d v_1^T) from
+// the small error d = v^ - v_1, which tilts each remaining eigenvector towards v_1
+// by lam_1 d_j / lam_j; the span of [V, V_D] is right, and projecting v^ out is
+// exact to O(lam_1 |d|^2).  One block per column; fixed-order block reductions.
+__global__ __launch_bounds__(256) void deflate_orth_kernel(float* __restrict__ V, int64_t ldv,
+                                                           int64_t d, int kc, int r) {
+  __shared__ float red[4][8];
+  __shared__ float coef[8];
+  const int j = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  float* v = V + (int64_t)j * ldv;
+  const float* vd = V + (int64_t)kc * ldv;
+  float dot[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dot[q] = 0.f;
+  for (int64_t i = tid; i < d; i += 256) {
+    const float x = v[i];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q < r) dot[q] = fmaf(vd[(int64_t)q * ldv + i], x, dot[q]);
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    float t = dot[q];
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == 0) red[w][q] = t;
+  }
+  __syncthreads();
+  if (tid < 8) coef[tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+  __syncthreads();
+  float nrm = 0.f;
+  for (int64_t i = tid; i < d; i += 256) {
+    float x = v[i];
+    for (int q = 0; q < r; ++q) x = fmaf(-coef[q], vd[(int64_t)q * ldv + i], x);
+    v[i] = x;
+    nrm = fmaf(x, x, nrm);
+  }
+  for (int o = 32; o > 0; o >>= 1) nrm += __shfl_xor(nrm, o, 64);
+  __syncthreads();
+  if (lane == 0) red[w][0] = nrm;
+  __syncthreads();
+  const float sc = rsqrtf(red[0][0] + red[1][0] + red[2][0] + red[3][0]);
+  for (int64_t i = tid; i < d; i += 256) v[i] *= sc;
+}
+
 size_t rr_small_shm(int p) {
   return (size_t)(2 * p * p + 7 * p + RT / 64 + 20) * sizeof(float);
 }
@@ -651,6 +697,13 @@ int cheb_step_launch(const RRBuffers& b, float* T, int64_t d, int p, float thr, 
   DEIG_REQUIRE(p % 16 == 0, "cheb_step: p=%d must be a multiple of 16", p);
   hipLaunchKernelGGL(cheb_step_kernel, dim3((unsigned)cdiv(d * (p / 4), 256)), dim3(256), 0,
                      stream, b.Z, T, d, p, b.lam, thr, alpha, cc, gamma);
+  DEIG_HIP_CHECK(hipGetLastError());
+  return DEIG_OK;
+}
+
+int deflate_orth_launch(float* V, int64_t ldv, int64_t d, int kc, int r, hipStream_t stream) {
+  DEIG_REQUIRE(r >= 1 && r <= 8 && kc >= 1, "deflate_orth: r=%d kc=%d out of range", r, kc);
+  hipLaunchKernelGGL(deflate_orth_kernel, dim3(kc), dim3(256), 0, stream, V, ldv, d, kc, r);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }
