@@ -9,9 +9,11 @@ runs on the GPU through the HIP hot path:
   top-k (the reference builds the d x d sigma_tilde and discards it; the notebook's
   server solve, raw line 306, is what is computed here - without forming d x d).
 
-Transport: the reference uses pika/RabbitMQ (out of scope).  ``broker_host`` names
-an in-process broker (``broker.py``) with the same channel API; requests and
-responses are the same JSON documents
+Transport: the reference uses pika/RabbitMQ (out of scope).  ``broker_host`` is
+either ``tcp://HOST:PORT`` - the socket broker of ``broker.py``, so ``--mode slave``
+and ``--mode master`` run as separate processes like the reference's CLI - or a
+name of an in-process broker with the same channel API; requests and responses
+are the same JSON documents
 (request ``{"rank": k, "batch": [lo, hi]}``, response
 ``{"batch": [lo, hi], "eigenspace": d x k nested list}``, distributed.py:49-52,
 :109-112).
@@ -251,19 +253,39 @@ def preprocess(data):
     return data.reshape(data.shape[:-2] + (-1,))
 
 
+def load_dataset(path):
+    """The reference's data (distributed.py:169-173) for the nodes.
+
+    A CIFAR batch directory (load_data.py:18-33) stays uint8 (N, 32, 32, 3): the
+    grayscale + flatten of :170-173 is fused into the exact integer covariance on
+    the GPU (linalg.sigma_hat_u8), which gives the correctly rounded value of the
+    reference's float64 result.  A ``.npy`` file (addition, for non-CIFAR data and
+    tests) is used as stored (loaded without pickle); a 4-D float array there gets
+    the reference's host preprocessing."""
+    import os
+    if os.path.isfile(path) and path.endswith(".npy"):
+        data = np.load(path, allow_pickle=False)
+    else:
+        from .load_data import load_CIFAR_10_data
+        data, filenames, labels = load_CIFAR_10_data(path)
+    if data.ndim == 4 and data.dtype != np.uint8:
+        data = preprocess(data)
+    return data
+
+
 def main(argv=None):
     parser = argparse.ArgumentParser(description="Multinode PCA")
     parser.add_argument("--mode", help="Mode to run script - slave, master or local")
-    parser.add_argument("--broker", help="Message broker name (in-process broker)")
+    parser.add_argument("--broker", help="Message broker: tcp://HOST:PORT (socket broker, separate "
+                        "processes; start it with python -m distributed_eigenspaces_amd.broker "
+                        "--serve HOST:PORT) or a name (in-process broker)")
     parser.add_argument("--rank", help="Approximation rank (only for master node")
     parser.add_argument("--batches", help="Total batches number")
     parser.add_argument("--data", default="cifar-10-batches-py", help="Path to dataset")
     args = parser.parse_args(argv)
     if args.broker is None:
         raise RuntimeError("Broker not specified")
-    from .load_data import load_CIFAR_10_data
-    data, filenames, labels = load_CIFAR_10_data(args.data)
-    data = preprocess(data)
+    data = load_dataset(args.data)
     if args.mode == "slave":
         return run_slave(args.broker, data)
     elif args.mode == "master":

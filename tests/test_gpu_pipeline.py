@@ -270,3 +270,16 @@ def test_streaming_oja_single_rank_matches_oracle(cuda):
     ref = ref_cpu.oja_stream([batches], V0.double().cpu().numpy(), eta, agg)
     assert ref_cpu.projector_distance(a.V.cpu().numpy(), ref) <= P_TOL
     assert ref_cpu.projector_distance(c.V.cpu().numpy(), ref) <= P_TOL
+
+
+def test_socket_two_process_protocol_gpu(tmp_path, cuda):
+    """The multi-process CLI with the real GPU nodes: ``--mode master`` and ``--mode
+    slave`` as separate processes over the socket broker (distributed.py:156-184),
+    against the reference's golden run (arrival order and results)."""
+    from tests.test_socket_broker import _run_pair
+    g, r, _ = _run_pair(tmp_path, "spiked_d128_k2_m5_ragged", [], timeout=240)
+    np.testing.assert_array_equal(r["ranges"], g["ranges"])
+    for i in range(len(g["ranges"])):
+        assert ref_cpu.projector_distance(r["worker_V"][i], g["worker_V"][i]) <= P_TOL
+    assert ref_cpu.projector_distance(r["server_V"], g["server_V"]) <= P_TOL
+    np.testing.assert_allclose(r["server_evals"], g["server_evals"], rtol=EV_TOL)
