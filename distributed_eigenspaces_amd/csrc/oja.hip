@@ -3,6 +3,8 @@
 // Not present in the reference (parity unpinned; judged by sin(theta) against
 // the one-shot float64 oracle and ref_cpu.oja_epoch).  Xb is read twice (Xb V
 // and Xb^T T), each pass a skinny GEMM at ~k/2 flop/B (HBM-bound for k <= 32).
+#include <stdlib.h>
+
 #include "deig_internal.hpp"
 
 namespace deig {
@@ -99,19 +101,232 @@ void launch_chol_rinv(const float* G, int k, int kp, float* Rinv, hipStream_t st
     hipLaunchKernelGGL(chol_rinv_kernel<64>, dim3(1), dim3(64), 0, st, G, k, kp, Rinv);
 }
 
+// ---------------------------------------------------------------- batch products
+// Per batch (b rows of X, d features, KP = 16 NB padded columns), two passes over Xb:
+//   oja_nn_kernel : T = Xb V          (b x KP row-major)
+//   oja_tn_kernel : Vc += c Xb^T T    (Vc: d x KP column-major work basis)
+// fp32 MFMA 16x16x4 (exact fp32 fma chains).  Both read Xb with float4 loads and
+// need no separate reduce kernel: NN gives each block 16 complete rows (K split
+// over its 8 waves, summed in LDS in wave order) and TN's row-slice partials are
+// summed by the last block to finish each feature block (fixed slice order:
+// deterministic), so a batch is exactly two launches.
+constexpr int NN_ROWS = 16, NN_THR = 512, NN_WAVES = NN_THR / 64;
+constexpr int TN_FEAT = 256, TN_THR = 256;  // 4 waves x 64 features
+
+// Lane (r = l & 15, g = l >> 4) loads Xb[r0 + r][16 c + 4 g .. + 3] and the B
+// fragments V[16 c + 4 g .. + 3][16 j + r] (column-major V: contiguous in k); MFMA
+// step s uses component s of both, i.e. k = 16 c + 4 g + s for lane group g - the
+// same permuted k on both operands, so the product is exact.
+template <int NB>
+__global__ __launch_bounds__(NN_THR) void oja_nn_kernel(const float* __restrict__ X, int64_t ldx,
+                                                       int64_t b, int64_t d, int64_t dpad,
+                                                       const float* __restrict__ Vc,
+                                                       float* __restrict__ T) {
+  constexpr int KP = 16 * NB;
+  __shared__ f32x4 red[NN_WAVES][NB][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int64_t r0 = (int64_t)blockIdx.x * NN_ROWS;
+  const int64_t row = r0 + r;
+  const bool rok = row < b;
+  const float* xr = X + (rok ? row : 0) * ldx + 4 * g;
+  const int64_t nch = d / 16;  // d % 16 == 0 (padded by the caller)
+  const int64_t c0 = nch * w / NN_WAVES, c1 = nch * (w + 1) / NN_WAVES;
+  f32x4 acc[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  const float* vb = Vc + (int64_t)r * dpad + 4 * g;
+  // U chunks per iteration: their loads are all issued before the MFMAs
+  constexpr int U = 4;
+  auto step = [&](const f32x4& a, const f32x4 (&bv)[NB]) {
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2], bv[j][s2], acc[j], 0, 0, 0);
+  };
+  int64_t c = c0;
+  for (; c + U <= c1; c += U) {
+    f32x4 a[U], bv[U][NB];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      a[u] = rok ? *reinterpret_cast<const f32x4*>(xr + 16 * (c + u)) : zero;
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        bv[u][j] = *reinterpret_cast<const f32x4*>(vb + (int64_t)16 * j * dpad + 16 * (c + u));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) step(a[u], bv[u]);
+  }
+  for (; c < c1; ++c) {
+    f32x4 bv[NB];
+    const f32x4 a = rok ? *reinterpret_cast<const f32x4*>(xr + 16 * c) : zero;
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+      bv[j] = *reinterpret_cast<const f32x4*>(vb + (int64_t)16 * j * dpad + 16 * c);
+    step(a, bv);
+  }
+#pragma unroll
+  for (int j = 0; j < NB; ++j) red[w][j][lane] = acc[j];
+  __syncthreads();
+  // C/D map: column = lane & 15, row = 4 (lane >> 4) + e
+  for (int idx = tid; idx < NB * 64; idx += NN_THR) {
+    const int j = idx >> 6, l = idx & 63;
+    f32x4 s = red[0][j][l];
+#pragma unroll
+    for (int ww = 1; ww < NN_WAVES; ++ww) s += red[ww][j][l];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t rr = r0 + 4 * (l >> 4) + e;
+      if (rr < b) T[rr * KP + 16 * j + (l & 15)] = s[e];
+    }
+  }
+}
+
+// grid (d / TN_FEAT, ns): block (fb, sl) covers features [256 fb, +256) and rows
+// [b sl / ns, b (sl + 1) / ns).  Lane (q = l & 15, g = l >> 4) of wave w loads
+// Xb[row + g][f0 + 64 w + 4 q .. + 3] (4 rows x 256 contiguous bytes per wave
+// instruction) and the A fragments T[row + g][16 j + q]; MFMA e uses component e:
+// B[k = g][col = q] = Xb[row + g][f0 + 64 w + 4 q + e], so accumulator (j, e)
+// holds output column 16 j + 4 (l >> 4) + reg of feature f0 + 64 w + 4 (l & 15) + e.
+// The partial tile goes to a slab; the last block of a feature block (arrival
+// counter) sums the ns slabs in slice order, adds Vc and stores Vc.
+template <int NB>
+__global__ __launch_bounds__(TN_THR) void oja_tn_kernel(const float* __restrict__ X, int64_t ldx,
+                                                       int64_t b, int64_t d, int64_t dpad,
+                                                       const float* __restrict__ T, float coef,
+                                                       float* __restrict__ Vc,
+                                                       float* __restrict__ part,
+                                                       unsigned* __restrict__ count) {
+  constexpr int KP = 16 * NB;
+  constexpr int TILE = TN_FEAT * KP;  // floats per slab
+  __shared__ unsigned last_flag;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int q = lane & 15, g = lane >> 4;
+  const int fb = blockIdx.x, sl = blockIdx.y, ns = gridDim.y;
+  const int64_t f0 = (int64_t)fb * TN_FEAT + 64 * w + 4 * q;
+  const int64_t k0 = b * sl / ns, k1 = b * (sl + 1) / ns;
+  f32x4 acc[NB][4];
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[j][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  const bool fok = f0 < d;
+  auto ld = [&](int64_t k, f32x4& x, float (&t)[NB]) {
+    const int64_t row = k + g;
+    const bool ok = row < k1;
+    x = (ok && fok) ? *reinterpret_cast<const f32x4*>(X + row * ldx + f0) : zero;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) t[j] = ok ? T[row * KP + 16 * j + q] : 0.f;
+  };
+  auto step = [&](const f32x4& x, const float (&t)[NB]) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc[j][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(t[j], x[e], acc[j][e], 0, 0, 0);
+  };
+  constexpr int U = 4;  // 4-row steps per iteration, loads issued first
+  int64_t k = k0;
+  for (; k + 4 * U <= k1; k += 4 * U) {
+    f32x4 x[U];
+    float t[U][NB];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ld(k + 4 * u, x[u], t[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) step(x[u], t[u]);
+  }
+  for (; k < k1; k += 4) {
+    f32x4 x;
+    float t[NB];
+    ld(k, x, t);
+    step(x, t);
+  }
+  // slab image: [feature (256)][column (KP)], this thread's 4 x 4 x NB values
+  float* slab = part + ((int64_t)fb * ns + sl) * TILE;
+  const int fl = 64 * w + 4 * q;
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      *reinterpret_cast<f32x4*>(slab + (fl + e) * KP + 16 * j + 4 * g) = acc[j][e];
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) last_flag = (atomicAdd(count + fb, 1u) == (unsigned)(ns - 1)) ? 1u : 0u;
+  __syncthreads();
+  if (!last_flag) return;
+  __threadfence();
+  // last block of this feature block: Vc[f][c] += coef * sum_sl slab (slice order)
+  const float* base = part + (int64_t)fb * ns * TILE;
+  for (int idx = tid; idx < TILE / 4; idx += TN_THR) {
+    f32x4 s = *reinterpret_cast<const f32x4*>(base + 4 * idx);
+    for (int u = 1; u < ns; ++u) s += *reinterpret_cast<const f32x4*>(base + (int64_t)u * TILE + 4 * idx);
+    const int f = (4 * idx) / KP, c = (4 * idx) % KP;
+    const int64_t feat = (int64_t)fb * TN_FEAT + f;
+    if (feat < d)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Vc[(int64_t)(c + e) * dpad + feat] += coef * s[e];
+  }
+  if (tid == 0) count[fb] = 0u;  // ready for the next batch (kernel boundary orders it)
+}
+
+// Column-major V (ldv, k columns) <-> the work basis Vc (d x KP column-major, zero
+// columns k .. KP-1; d padded to a multiple of 256 rows with zeros).
+__global__ __launch_bounds__(256) void v_to_work(const float* __restrict__ V, int64_t ldv, int64_t d,
+                                                 int64_t dpad, int k, int kp, float* __restrict__ Vc) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= dpad * kp) return;
+  const int j = (int)(idx / dpad);
+  const int64_t r = idx - (int64_t)j * dpad;
+  Vc[idx] = (j < k && r < d) ? V[r + (int64_t)j * ldv] : 0.f;
+}
+
+__global__ __launch_bounds__(256) void work_to_rowpad(const float* __restrict__ Vc, int64_t dpad,
+                                                      int64_t d, int kp, float* __restrict__ Vr) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= d * kp) return;
+  const int64_t r = idx / kp;
+  const int j = (int)(idx - r * kp);
+  Vr[idx] = Vc[(int64_t)j * dpad + r];
+}
+
+__global__ __launch_bounds__(256) void rowpad_to_work(const float* __restrict__ Vr, int64_t d,
+                                                      int64_t dpad, int kp, float* __restrict__ Vc) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= d * kp) return;
+  const int64_t r = idx / kp;
+  const int j = (int)(idx - r * kp);
+  Vc[(int64_t)j * dpad + r] = Vr[idx];
+}
+
 struct OjaWs {
-  float *Vr, *Vr2, *T, *G, *Rinv, *slab;
+  float *Vr, *Vr2, *T, *G, *Rinv, *slab, *Vc, *part;
+  unsigned* count;
   size_t slab_bytes;
 };
+
+int tn_slices(int64_t b, int64_t d) {
+  const int64_t nfb = cdiv(d, TN_FEAT);
+  int64_t ns = cdiv(2 * num_cus(), nfb);  // ~2 blocks per CU
+  const int64_t cap = cdiv(b, 64);        // >= 64 rows per slice
+  if (ns > cap) ns = cap;
+  return (int)(ns < 1 ? 1 : ns);
+}
 
 OjaWs carve_oja(void* ws, size_t cap, int64_t b, int64_t d, int kp, size_t* total) {
   Carve c(ws, cap);
   OjaWs o;
+  const int64_t dpad = cdiv(d, TN_FEAT) * TN_FEAT;
   o.Vr = c.take<float>((size_t)d * kp);
   o.Vr2 = c.take<float>((size_t)d * kp);
   o.T = c.take<float>((size_t)b * kp);
   o.G = c.take<float>((size_t)kp * kp);
   o.Rinv = c.take<float>((size_t)kp * kp);
+  o.Vc = c.take<float>((size_t)dpad * kp);
+  o.part = c.take<float>((size_t)(dpad / TN_FEAT) * tn_slices(b, d) * TN_FEAT * kp);
+  o.count = c.take<unsigned>((size_t)(dpad / TN_FEAT));
   size_t sb = skinny_workspace_bytes(b, kp, d);
   size_t s2 = skinny_workspace_bytes(d, kp, b);
   size_t s3 = skinny_workspace_bytes(kp, kp, d);
@@ -163,6 +378,62 @@ size_t oja_workspace_bytes(int64_t b, int64_t d, int k) {
 // invertible k x k factor, so the span after every batch equals the one of
 // per-batch orthonormalisation (ref_cpu.oja_epoch); deferring it only lets the
 // column norms grow by ~(1 + eta lambda_max)^orth_every in between.
+template <int NB>
+void launch_batch(const OjaWs& o, const float* Xb, int64_t ldx, int64_t b, int64_t d, int64_t dpad,
+                  float coef, int ns, hipStream_t st) {
+  hipLaunchKernelGGL(oja_nn_kernel<NB>, dim3((unsigned)cdiv(b, NN_ROWS)), dim3(NN_THR), 0, st, Xb,
+                     ldx, b, d, dpad, o.Vc, o.T);
+  hipLaunchKernelGGL(oja_tn_kernel<NB>, dim3((unsigned)(dpad / TN_FEAT), (unsigned)ns),
+                     dim3(TN_THR), 0, st, Xb, ldx, b, d, dpad, o.T, coef, o.Vc, o.part, o.count);
+}
+
+// The v2 path (d % 16 == 0; DEIG_OJA_KERNEL=1 selects the v1 skinny-GEMM path):
+// per batch oja_nn_kernel + oja_tn_kernel on the column-major work basis Vc; the
+// basis is copied to the row-padded layout of cholqr2 only at orthonormalisation.
+int oja_steps_v2(const float* X, int64_t nb, int64_t b, int64_t d, int64_t ldx, float eta,
+                 float* V, int k, int64_t ldv, int orth_every, const OjaWs& o, int kp,
+                 hipStream_t st) {
+  const int64_t dpad = cdiv(d, TN_FEAT) * TN_FEAT;
+  const int ns = tn_slices(b, d);
+  DEIG_HIP_CHECK(hipMemsetAsync(o.count, 0, sizeof(unsigned) * (dpad / TN_FEAT), st));
+  hipLaunchKernelGGL(v_to_work, dim3((unsigned)cdiv(dpad * kp, 256)), dim3(256), 0, st, V, ldv, d,
+                     dpad, k, kp, o.Vc);
+  DEIG_HIP_CHECK(hipGetLastError());
+  const float coef = eta / (float)b;
+  int rc;
+  for (int64_t i = 0; i < nb; ++i) {
+    const float* Xb = X + i * b * ldx;
+    switch (kp / 16) {
+      case 1: launch_batch<1>(o, Xb, ldx, b, d, dpad, coef, ns, st); break;
+      case 2: launch_batch<2>(o, Xb, ldx, b, d, dpad, coef, ns, st); break;
+      case 3: launch_batch<3>(o, Xb, ldx, b, d, dpad, coef, ns, st); break;
+      default: launch_batch<4>(o, Xb, ldx, b, d, dpad, coef, ns, st); break;
+    }
+    DEIG_HIP_CHECK(hipGetLastError());
+    if ((i + 1) % orth_every == 0 || i + 1 == nb) {
+      hipLaunchKernelGGL(work_to_rowpad, dim3((unsigned)cdiv(d * kp, 256)), dim3(256), 0, st, o.Vc,
+                         dpad, d, kp, o.Vr);
+      if ((rc = cholqr2(o, d, k, kp, st))) return rc;
+      hipLaunchKernelGGL(rowpad_to_work, dim3((unsigned)cdiv(d * kp, 256)), dim3(256), 0, st, o.Vr,
+                         d, dpad, kp, o.Vc);
+      DEIG_HIP_CHECK(hipGetLastError());
+    }
+  }
+  hipLaunchKernelGGL(rowpad_to_col, dim3((unsigned)cdiv(d * k, 256)), dim3(256), 0, st, o.Vr, d, k,
+                     kp, V, ldv);
+  DEIG_HIP_CHECK(hipGetLastError());
+  return DEIG_OK;
+}
+
+int oja_kernel_version() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DEIG_OJA_KERNEL");
+    v = (e && atoi(e) == 1) ? 1 : 2;
+  }
+  return v;
+}
+
 int oja_steps_launch(const float* X, int64_t nb, int64_t b, int64_t d, int64_t ldx, float eta,
                      float* V, int k, int64_t ldv, int orth_every, void* ws, size_t ws_bytes,
                      hipStream_t st) {
@@ -176,6 +447,8 @@ int oja_steps_launch(const float* X, int64_t nb, int64_t b, int64_t d, int64_t l
   OjaWs o = carve_oja(ws, ws_bytes, b, d, kp, &total);
   if (!ws || total > ws_bytes)
     return fail(DEIG_EWORKSPACE, "oja: workspace %zu < %zu", ws_bytes, total);
+  if (d % 16 == 0 && ldx % 4 == 0 && aligned16(X) && oja_kernel_version() == 2)
+    return oja_steps_v2(X, nb, b, d, ldx, eta, V, k, ldv, orth_every, o, kp, st);
   int rc;
   hipLaunchKernelGGL(col_to_rowpad, dim3((unsigned)cdiv(d * kp, 256)), dim3(256), 0, st, V, ldv, d,
                      k, kp, o.Vr);
