@@ -110,8 +110,10 @@ void launch_chol_rinv(const float* G, int k, int kp, float* Rinv, hipStream_t st
 // over its 8 waves, summed in LDS in wave order) and TN's row-slice partials are
 // summed by the last block to finish each feature block (fixed slice order:
 // deterministic), so a batch is exactly two launches.
-constexpr int NN_ROWS = 16, NN_THR = 512, NN_WAVES = NN_THR / 64;
-constexpr int TN_FEAT = 256, TN_THR = 256;  // 4 waves x 64 features
+constexpr int NN_ROWS = 16, NN_THR = 1024, NN_WAVES = NN_THR / 64;
+// TN: a block = TN_WAVES waves on one 64-feature tile, each wave a row sub-slice;
+// the waves' partial tiles are summed in LDS (wave order) before the block's slab.
+constexpr int TN_FEAT = 64, TN_WAVES = 8, TN_THR = 64 * TN_WAVES;
 
 // Lane (r = l & 15, g = l >> 4) loads Xb[r0 + r][16 c + 4 g .. + 3] and the B
 // fragments V[16 c + 4 g .. + 3][16 j + r] (column-major V: contiguous in k); MFMA
@@ -184,14 +186,15 @@ __global__ __launch_bounds__(NN_THR) void oja_nn_kernel(const float* __restrict_
   }
 }
 
-// grid (d / TN_FEAT, ns): block (fb, sl) covers features [256 fb, +256) and rows
-// [b sl / ns, b (sl + 1) / ns).  Lane (q = l & 15, g = l >> 4) of wave w loads
-// Xb[row + g][f0 + 64 w + 4 q .. + 3] (4 rows x 256 contiguous bytes per wave
-// instruction) and the A fragments T[row + g][16 j + q]; MFMA e uses component e:
-// B[k = g][col = q] = Xb[row + g][f0 + 64 w + 4 q + e], so accumulator (j, e)
-// holds output column 16 j + 4 (l >> 4) + reg of feature f0 + 64 w + 4 (l & 15) + e.
-// The partial tile goes to a slab; the last block of a feature block (arrival
-// counter) sums the ns slabs in slice order, adds Vc and stores Vc.
+// grid (dpad / 64, ns): block (fb, sl) covers features [64 fb, +64) and rows
+// [b sl / ns, b (sl + 1) / ns), split over its TN_WAVES waves.  Lane (q = l & 15,
+// g = l >> 4) loads Xb[row + g][f0 + 4 q .. + 3] (4 rows x 256 contiguous bytes
+// per wave instruction) and the A fragments T[row + g][16 j + q]; MFMA e uses
+// component e: B[k = g][col = q] = Xb[row + g][f0 + 4 q + e], so accumulator (j, e)
+// holds output column 16 j + 4 (l >> 4) + reg of feature f0 + 4 (l & 15) + e.
+// The waves' tiles are summed in LDS (wave order), the block's tile goes to a slab,
+// and the last block of a feature tile (arrival counter) sums the ns slabs in slice
+// order with independent loads, adds Vc and stores Vc.
 template <int NB>
 __global__ __launch_bounds__(TN_THR) void oja_tn_kernel(const float* __restrict__ X, int64_t ldx,
                                                        int64_t b, int64_t d, int64_t dpad,
@@ -200,13 +203,15 @@ __global__ __launch_bounds__(TN_THR) void oja_tn_kernel(const float* __restrict_
                                                        float* __restrict__ part,
                                                        unsigned* __restrict__ count) {
   constexpr int KP = 16 * NB;
-  constexpr int TILE = TN_FEAT * KP;  // floats per slab
+  constexpr int TILE = TN_FEAT * KP;  // floats per slab: [feature 64][column KP]
+  __shared__ f32x4 red[TN_WAVES][NB * 4][64];
   __shared__ unsigned last_flag;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int q = lane & 15, g = lane >> 4;
   const int fb = blockIdx.x, sl = blockIdx.y, ns = gridDim.y;
-  const int64_t f0 = (int64_t)fb * TN_FEAT + 64 * w + 4 * q;
-  const int64_t k0 = b * sl / ns, k1 = b * (sl + 1) / ns;
+  const int64_t f0 = (int64_t)fb * TN_FEAT + 4 * q;
+  const int64_t s0 = b * sl / ns, s1 = b * (sl + 1) / ns;
+  const int64_t k0 = s0 + (s1 - s0) * w / TN_WAVES, k1 = s0 + (s1 - s0) * (w + 1) / TN_WAVES;
   f32x4 acc[NB][4];
 #pragma unroll
   for (int j = 0; j < NB; ++j)
@@ -228,7 +233,7 @@ __global__ __launch_bounds__(TN_THR) void oja_tn_kernel(const float* __restrict_
       for (int e = 0; e < 4; ++e)
         acc[j][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(t[j], x[e], acc[j][e], 0, 0, 0);
   };
-  constexpr int U = 4;  // 4-row steps per iteration, loads issued first
+  constexpr int U = 8;  // 4-row steps per iteration, loads issued first
   int64_t k = k0;
   for (; k + 4 * U <= k1; k += 4 * U) {
     f32x4 x[U];
@@ -244,30 +249,45 @@ __global__ __launch_bounds__(TN_THR) void oja_tn_kernel(const float* __restrict_
     ld(k, x, t);
     step(x, t);
   }
-  // slab image: [feature (256)][column (KP)], this thread's 4 x 4 x NB values
-  float* slab = part + ((int64_t)fb * ns + sl) * TILE;
-  const int fl = 64 * w + 4 * q;
 #pragma unroll
   for (int j = 0; j < NB; ++j)
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      *reinterpret_cast<f32x4*>(slab + (fl + e) * KP + 16 * j + 4 * g) = acc[j][e];
+    for (int e = 0; e < 4; ++e) red[w][4 * j + e][lane] = acc[j][e];
+  __syncthreads();
+  // block tile -> slab; thread (j, e, l) sums the TN_WAVES waves in order
+  float* slab = part + ((int64_t)fb * ns + sl) * TILE;
+  for (int idx = tid; idx < NB * 4 * 64; idx += TN_THR) {
+    const int je = idx >> 6, l = idx & 63;
+    f32x4 sacc = red[0][je][l];
+#pragma unroll
+    for (int ww = 1; ww < TN_WAVES; ++ww) sacc += red[ww][je][l];
+    const int j = je >> 2, e = je & 3;
+    *reinterpret_cast<f32x4*>(slab + (4 * (l & 15) + e) * KP + 16 * j + 4 * (l >> 4)) = sacc;
+  }
   __threadfence();
   __syncthreads();
   if (tid == 0) last_flag = (atomicAdd(count + fb, 1u) == (unsigned)(ns - 1)) ? 1u : 0u;
   __syncthreads();
   if (!last_flag) return;
   __threadfence();
-  // last block of this feature block: Vc[f][c] += coef * sum_sl slab (slice order)
+  // last block of this feature tile: Vc[f][c] += coef * sum_sl slab (slice order)
   const float* base = part + (int64_t)fb * ns * TILE;
   for (int idx = tid; idx < TILE / 4; idx += TN_THR) {
-    f32x4 s = *reinterpret_cast<const f32x4*>(base + 4 * idx);
-    for (int u = 1; u < ns; ++u) s += *reinterpret_cast<const f32x4*>(base + (int64_t)u * TILE + 4 * idx);
+    f32x4 sv[8];
+    f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
+    for (int u0 = 0; u0 < ns; u0 += 8) {  // 8 independent loads in flight
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (u0 + u < ns) sv[u] = *reinterpret_cast<const f32x4*>(base + (int64_t)(u0 + u) * TILE + 4 * idx);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (u0 + u < ns) sacc += sv[u];
+    }
     const int f = (4 * idx) / KP, c = (4 * idx) % KP;
     const int64_t feat = (int64_t)fb * TN_FEAT + f;
     if (feat < d)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) Vc[(int64_t)(c + e) * dpad + feat] += coef * s[e];
+      for (int e = 0; e < 4; ++e) Vc[(int64_t)(c + e) * dpad + feat] += coef * sacc[e];
   }
   if (tid == 0) count[fb] = 0u;  // ready for the next batch (kernel boundary orders it)
 }
@@ -307,10 +327,14 @@ struct OjaWs {
   size_t slab_bytes;
 };
 
+// Row slices per feature tile: about 2 waves per SIMD over the grid, >= 8 rows per
+// wave (DEIG_OJA_TN_SLICES overrides, for tuning).
 int tn_slices(int64_t b, int64_t d) {
+  if (const char* e = getenv("DEIG_OJA_TN_SLICES"))
+    if (atoi(e) > 0) return atoi(e);
   const int64_t nfb = cdiv(d, TN_FEAT);
-  int64_t ns = cdiv(2 * num_cus(), nfb);  // ~2 blocks per CU
-  const int64_t cap = cdiv(b, 64);        // >= 64 rows per slice
+  int64_t ns = cdiv(2 * 4 * num_cus(), nfb * TN_WAVES);
+  const int64_t cap = cdiv(b, 8 * TN_WAVES);
   if (ns > cap) ns = cap;
   return (int)(ns < 1 ? 1 : ns);
 }
