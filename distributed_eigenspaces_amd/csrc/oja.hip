@@ -42,49 +42,73 @@ __device__ __forceinline__ float lane_bcast(float v, int src) {
 template <int KP>
 __global__ __launch_bounds__(64) void chol_rinv_kernel(const float* __restrict__ G, int k, int kp,
                                                        float* __restrict__ Rinv) {
-  const int c = threadIdx.x;  // column owned by this lane
-  const bool live = c < k;
-  float A[KP];
+  // One wave; lane r keeps row r of the matrix in registers (static indices: the
+  // loops over KP are unrolled).  G is extended to KP x KP by the identity beyond k
+  // (its Cholesky factor and inverse are then block-diagonal with an identity
+  // block), so nothing depends on the runtime k.  Columns / rows of L are exchanged
+  // through LDS with broadcast ds_read_b128 (all lanes read the same address):
+  // per Cholesky step one column, for the inverse the finished rows.  (A version
+  // broadcasting with v_readlane took ~23 us for k = 32: ~1000 readlanes with their
+  // hazard s_nops, plus runtime-k branches.)
+  __shared__ __attribute__((aligned(16))) float col[KP];
+  __shared__ __attribute__((aligned(16))) float Ls[KP][KP];
+  const int r = threadIdx.x;  // row owned by this lane (lanes >= KP idle but in step)
+  const bool live = r < KP;
+  float a[KP];
 #pragma unroll
-  for (int i = 0; i < KP; ++i) A[i] = (live && i < k) ? G[i * kp + c] : 0.f;
-  const float ref0 = fabsf(lane_bcast(A[0], 0)) > 0.f ? fabsf(lane_bcast(A[0], 0)) : 1.f;
-  float dinv[KP];  // 1 / L[j][j], uniform
-  // Right-looking Cholesky: after step j, A[j] (lane c) = L[c][j] for c >= j.
+  for (int c = 0; c < KP; ++c) {
+    const bool in = r < k && c < k;
+    a[c] = in ? G[r * kp + c] : (r == c ? 1.f : 0.f);
+  }
+  const float ref0 = fmaxf(fabsf(__shfl(a[0], 0, 64)), 1e-30f);
+  float dinv[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) {
-    if (j < k) {
-      float v = lane_bcast(A[j], j);
-      if (!(v > 1e-12f * ref0)) v = 1e-12f * ref0;
-      const float ljj = sqrtf(v);
-      dinv[j] = 1.0f / ljj;
-      const float l = (c == j) ? ljj : (c > j ? A[j] * dinv[j] : 0.f);
-      A[j] = l;
+    // pivot A[j][j] from lane j; L[r][j] = A[r][j] / L[j][j] for r > j
+    const float v = fmaxf(__shfl(a[j], j, 64), 1e-12f * ref0);
+    const float ljj = sqrtf(v);
+    dinv[j] = 1.0f / ljj;
+    const float l = (r == j) ? ljj : (r > j ? a[j] * dinv[j] : 0.f);
+    a[j] = l;
+    if (live) col[r] = l;
+    __syncthreads();
+    // trailing update of this lane's row: A[r][c] -= L[r][j] L[c][j]  (c > j)
 #pragma unroll
-      for (int i = j + 1; i < KP; ++i)
-        if (i < k) A[i] = fmaf(-lane_bcast(l, i), l, A[i]);  // A[i][c] -= L[i][j] L[c][j]
-    } else {
-      dinv[j] = 0.f;
+    for (int c4 = (j + 1) / 4; c4 < KP / 4; ++c4) {
+      const f32x4 lc = *reinterpret_cast<const f32x4*>(col + 4 * c4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (4 * c4 + e > j) a[4 * c4 + e] = fmaf(-l, lc[e], a[4 * c4 + e]);
     }
+    __syncthreads();
   }
-  // Lane r now holds row r of L in A[0 .. r].  X = L^-1 column c: for i = 0..k-1,
-  // X[i] = (delta_ic - sum_{t < i} L[i][t] X[t]) / L[i][i].
+  // lane r holds row r of L in a[0 .. r] (zeros above the diagonal)
+  if (live)
+#pragma unroll
+    for (int c4 = 0; c4 < KP / 4; ++c4)
+      *reinterpret_cast<f32x4*>(&Ls[r][4 * c4]) =
+          f32x4{a[4 * c4], a[4 * c4 + 1], a[4 * c4 + 2], a[4 * c4 + 3]};
+  __syncthreads();
+  // X = L^-1, lane c = column c: X[i] = (delta_ic - sum_{t < i} L[i][t] X[t]) / L[i][i]
+  const int c = r;
   float X[KP];
 #pragma unroll
   for (int i = 0; i < KP; ++i) {
-    if (i < k) {
-      float s = (c == i) ? 1.0f : 0.0f;
+    float sacc = (c == i) ? 1.0f : 0.0f;
 #pragma unroll
-      for (int t = 0; t < i; ++t) s = fmaf(-lane_bcast(A[t], i), X[t], s);
-      X[i] = s * dinv[i];
-    } else {
-      X[i] = 0.f;
+    for (int t4 = 0; t4 < (i + 3) / 4; ++t4) {
+      const f32x4 li = *reinterpret_cast<const f32x4*>(&Ls[i][4 * t4]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (4 * t4 + e < i) sacc = fmaf(-li[e], X[4 * t4 + e], sacc);
     }
+    X[i] = sacc * dinv[i];
   }
-  // Rinv = L^-T: Rinv[c][i] = X[i][c] (lane c); rows / columns >= k are zero.
+  // Rinv = L^-T: Rinv[c][i] = X[i][c] (lane c); zero outside the k x k block
   if (c < kp) {
 #pragma unroll
     for (int i = 0; i < KP; ++i)
-      if (i < kp) Rinv[c * kp + i] = (live && i < k) ? X[i] : 0.f;
+      if (i < kp) Rinv[c * kp + i] = (c < k && i < k) ? X[i] : 0.f;
   }
 }
 
@@ -125,14 +149,15 @@ OjaWs carve_oja(void* ws, size_t cap, int64_t b, int64_t d, int kp, size_t* tota
   return o;
 }
 
-// Cholesky-QR of the row-padded d x kp basis in o.Vr (o.Vr2 is scratch) with
+// Cholesky-QR of the row-padded d x kp basis `in` (`scratch` has the same size) with
 // `passes` passes (2 = CholQR2, orthonormal to fp32 rounding; 1 = one pass, used
 // between batches where only the span and a bounded condition number matter);
-// the result is back in o.Vr (a buffer swap per pass, copied back if odd).
-int cholqr(const OjaWs& o, int64_t d, int k, int kp, hipStream_t st, int passes) {
+// the result is in *result (in or scratch: one buffer swap per pass).
+int cholqr(float* in, float* scratch, const OjaWs& o, int64_t d, int k, int kp, hipStream_t st,
+           int passes, float** result) {
   int rc;
-  float* cur = o.Vr;
-  float* nxt = o.Vr2;
+  float* cur = in;
+  float* nxt = scratch;
   for (int pass = 0; pass < passes; ++pass) {
     if ((rc = skinny_launch(true, cur, kp, cur, kp, o.G, kp, kp, kp, d, 1.f, 0.f, o.slab,
                             o.slab_bytes, st)))
@@ -146,8 +171,7 @@ int cholqr(const OjaWs& o, int64_t d, int k, int kp, hipStream_t st, int passes)
     cur = nxt;
     nxt = t;
   }
-  if (cur != o.Vr)
-    DEIG_HIP_CHECK(hipMemcpyAsync(o.Vr, cur, sizeof(float) * d * kp, hipMemcpyDeviceToDevice, st));
+  *result = cur;
   return DEIG_OK;
 }
 
@@ -181,28 +205,33 @@ int oja_steps_launch(const float* X, int64_t nb, int64_t b, int64_t d, int64_t l
   if (!ws || total > ws_bytes)
     return fail(DEIG_EWORKSPACE, "oja: workspace %zu < %zu", ws_bytes, total);
   int rc;
+  // the basis lives in `cur` (o.Vr or o.Vr2: each CholQR pass swaps the two)
+  float* cur = o.Vr;
+  float* spare = o.Vr2;
   hipLaunchKernelGGL(col_to_rowpad, dim3((unsigned)cdiv(d * kp, 256)), dim3(256), 0, st, V, ldv, d,
-                     k, kp, o.Vr);
+                     k, kp, cur);
   DEIG_HIP_CHECK(hipGetLastError());
   for (int64_t i = 0; i < nb; ++i) {
     const float* Xb = X + i * b * ldx;
     // T = Xb V
-    if ((rc = skinny_launch(false, Xb, ldx, o.Vr, kp, o.T, kp, b, kp, d, 1.f, 0.f, o.slab,
+    if ((rc = skinny_launch(false, Xb, ldx, cur, kp, o.T, kp, b, kp, d, 1.f, 0.f, o.slab,
                             o.slab_bytes, st)))
       return rc;
     // V += eta/b * Xb^T T
-    if ((rc = skinny_launch(true, Xb, ldx, o.T, kp, o.Vr, kp, d, kp, b, eta / (float)b, 1.f,
+    if ((rc = skinny_launch(true, Xb, ldx, o.T, kp, cur, kp, d, kp, b, eta / (float)b, 1.f,
                             o.slab, o.slab_bytes, st)))
       return rc;
     // intermediate re-orthonormalisations only bound the basis' condition number
     // (the span is what the update carries): one CholQR pass; the last one is CholQR2
-    if (i + 1 == nb) {
-      if ((rc = cholqr(o, d, k, kp, st, 2))) return rc;
-    } else if ((i + 1) % orth_every == 0) {
-      if ((rc = cholqr(o, d, k, kp, st, 1))) return rc;
+    const int passes = (i + 1 == nb) ? 2 : ((i + 1) % orth_every == 0 ? 1 : 0);
+    if (passes) {
+      float* res = cur;
+      if ((rc = cholqr(cur, spare, o, d, k, kp, st, passes, &res))) return rc;
+      spare = res == cur ? spare : cur;
+      cur = res;
     }
   }
-  hipLaunchKernelGGL(rowpad_to_col, dim3((unsigned)cdiv(d * k, 256)), dim3(256), 0, st, o.Vr, d, k,
+  hipLaunchKernelGGL(rowpad_to_col, dim3((unsigned)cdiv(d * k, 256)), dim3(256), 0, st, cur, d, k,
                      kp, V, ldv);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;

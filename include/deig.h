@@ -130,10 +130,17 @@ size_t deig_sym_apply_workspace(int64_t d, int p, int algo);
  * (scipy.linalg.eigh(S, eigvals=(d-k, d-1))[1]  ->  LAPACK dsyevr), plus the
  * eigenvalues ([0] of the same call) as a side output.
  * Block subspace iteration with Rayleigh-Ritz on a p-dimensional subspace
- * (k <= p <= 128, p % 16 == 0, p <= d).  Q0 (d x k0 column-major, ldq0) is an
- * optional warm start (NULL / k0 = 0 -> deterministic pseudo-random start).
- * Stops when max_j ||S v_j - lambda_j v_j|| <= tol * |lambda_max| or the
- * residual stagnates, after at most max_sweeps sweeps.
+ * (k <= p <= 128, p % 16 == 0, p <= d); between Rayleigh-Ritz steps a scaled
+ * Chebyshev filter on [0, c] (c from the Ritz values; power steps while the
+ * residual is above 1e-2) - S must be positive semi-definite, as covariances and
+ * projector averages are.  When theta_1 >= 64 theta_k (an uncentered covariance's
+ * mean direction), a second stage iterates the other pairs on S - V_D L_D V_D^T
+ * (fp32 products S q would otherwise lose their digits to cancellation).  Q0
+ * (d x k0 column-major, ldq0) is an optional warm start (NULL / k0 = 0 ->
+ * deterministic pseudo-random start).  Stops when
+ * max_j ||S v_j - lambda_j v_j|| <= tol * |lambda_max| (or the residual stalls
+ * within 4 tol / 2e-6 of it, the fp32 floor); returns DEIG_NOT_CONVERGED after
+ * max_sweeps sweeps, or earlier when it stalls above that floor.
  * Outputs: V (d x k col-major, ldv), evals (k, ascending), *sweeps_out,
  * *resid_out = final max relative residual (host pointers, may be NULL). */
 int deig_topk_sym_f32(const float* S, int64_t d, int64_t lds, int k, int p,
