@@ -497,13 +497,22 @@ def run_oneshot(args, cfg, world, rank, dev):
     # HBM-side bytes per covariance launch from the separate rocprofv3 PMC passes
     # (FETCH_SIZE / WRITE_SIZE, gfx950 corrections; tools/profile_round.sh) of this
     # same kernel and shard: tools/ travels to the GPU box, profiles/ does not.
-    traffic = None
+    # The measurement is bound to the kernel it describes: it is reported only while
+    # the covariance sources hash as they did when tools/profile_round.sh ran.
+    traffic, traffic_note = None, None
     pmc = os.path.join(ROOT, "tools", f"pmc_syrk_{args.config}_{algo}.json")
     if os.path.exists(pmc) and not args.rows:
         try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+            rec = json.load(open(pmc))
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            from pmc_traffic import source_sha256
+            if rec.get("source_sha256") == source_sha256():
+                traffic = rec.get("hbm_bytes_per_launch")
+                traffic_note = rec.get("measured")
+            else:
+                traffic_note = "stale: kernel sources changed since the PMC passes"
+        except Exception as e:  # pragma: no cover
+            traffic_note = f"unreadable ({e})"
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_oneshot(X, ni, W, k, min(args.cpu_sample, ni))
@@ -520,9 +529,11 @@ def run_oneshot(args, cfg, world, rank, dev):
                         "peak": peak / 1e12, "unit": "TFLOP/s", "frac": achieved / peak,
                         "traffic": traffic,
                         "traffic_source": (f"tools/pmc_syrk_{args.config}_{algo}.json (rocprofv3 "
-                                           "FETCH_SIZE x2 + WRITE_SIZE, separate passes; "
-                                           "fabric-side L2 misses incl. Infinity-Cache hits: an "
-                                           "upper bound on HBM bytes)") if traffic else None,
+                                           "FETCH_SIZE x2 + WRITE_SIZE, separate passes of this "
+                                           "kernel source (sha256-checked); fabric-side L2 misses "
+                                           "incl. Infinity-Cache hits: an upper bound on HBM "
+                                           f"bytes; {traffic_note})") if traffic else traffic_note,
+                        "traffic_vs_algorithmic": (traffic / (4.0 * ni * d)) if traffic else None,
                         "algorithmic": algorithmic, "launch_ms": syrk_ms,
                         "fp32_equiv_tflops": flops / (syrk_ms * 1e-3) / 1e12,
                         "fp32_mfma_peak": FP32_MFMA_PEAK / 1e12, "fp32_kernel": fp32_kernel}

@@ -11,9 +11,22 @@ usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> <n> <d> <l
 import collections
 import csv
 import glob
+import hashlib
 import json
+import os
 import re
 import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def source_sha256():
+    """Hash of the covariance kernel sources the measurement describes (bench.py
+    reports the traffic only while the sources still hash the same)."""
+    h = hashlib.sha256()
+    for f in ("syrk_split.hip", "deig_internal.hpp"):
+        h.update(open(os.path.join(ROOT, "distributed_eigenspaces_amd", "csrc", f), "rb").read())
+    return h.hexdigest()
 
 KERNELS = ["split_kernel", "syrks_kernel", "syrks_reduce_kernel", "diag_corr_kernel",
            "tile_order_kernel", "syrk_kernel", "syrk_reduce_kernel"]
@@ -55,6 +68,7 @@ res = {
     "caveat": "fabric-side L2 miss counters: Infinity-Cache hits included (upper bound on HBM bytes)",
     "passes": ["rocprofv3 --pmc FETCH_SIZE --output-format csv -- python3 tools/run_syrk_once.py",
                "rocprofv3 --pmc WRITE_SIZE --output-format csv -- python3 tools/run_syrk_once.py"],
+    "source_sha256": source_sha256(),
 }
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
