@@ -503,12 +503,12 @@ def run_oneshot(args, cfg, world, rank, dev):
     pmc = os.path.join(ROOT, "tools", f"pmc_syrk_{args.config}_{algo}.json")
     if os.path.exists(pmc) and not args.rows:
         try:
-            rec = json.load(open(pmc))
+            pmc_rec = json.load(open(pmc))
             sys.path.insert(0, os.path.join(ROOT, "tools"))
             from pmc_traffic import source_sha256
-            if rec.get("source_sha256") == source_sha256():
-                traffic = rec.get("hbm_bytes_per_launch")
-                traffic_note = rec.get("measured")
+            if pmc_rec.get("source_sha256") == source_sha256():
+                traffic = pmc_rec.get("hbm_bytes_per_launch")
+                traffic_note = pmc_rec.get("measured")
             else:
                 traffic_note = "stale: kernel sources changed since the PMC passes"
         except Exception as e:  # pragma: no cover

@@ -52,23 +52,28 @@ def per_kernel_last(dirpath, counter):
     return last
 
 
-fetch_dir, write_dir, out, n, d, label = sys.argv[1:7]
-n, d = int(n), int(d)
-fk = per_kernel_last(fetch_dir, "FETCH_SIZE")
-wk = per_kernel_last(write_dir, "WRITE_SIZE")
-per = {k: {"read_bytes": fk.get(k, 0.0) * 1024 * 2, "write_bytes": wk.get(k, 0.0) * 1024}
-       for k in sorted(set(fk) | set(wk))}
-rd = sum(v["read_bytes"] for v in per.values())
-wr = sum(v["write_bytes"] for v in per.values())
-res = {
-    "op": label, "config": f"n={n}, d={d} (one covariance launch)",
-    "per_kernel": per, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
-    "hbm_bytes_per_launch": rd + wr, "algorithmic_bytes_per_launch": 4 * n * d,
-    "correction": "FETCH_SIZE x 1024 x 2 (gfx950 half-count of 16-B/lane reads), WRITE_SIZE x 1024",
-    "caveat": "fabric-side L2 miss counters: Infinity-Cache hits included (upper bound on HBM bytes)",
-    "passes": ["rocprofv3 --pmc FETCH_SIZE --output-format csv -- python3 tools/run_syrk_once.py",
-               "rocprofv3 --pmc WRITE_SIZE --output-format csv -- python3 tools/run_syrk_once.py"],
-    "source_sha256": source_sha256(),
-}
-json.dump(res, open(out, "w"), indent=1)
-print(json.dumps(res, indent=1))
+def main():
+    fetch_dir, write_dir, out, n, d, label = sys.argv[1:7]
+    n, d = int(n), int(d)
+    fk = per_kernel_last(fetch_dir, "FETCH_SIZE")
+    wk = per_kernel_last(write_dir, "WRITE_SIZE")
+    per = {k: {"read_bytes": fk.get(k, 0.0) * 1024 * 2, "write_bytes": wk.get(k, 0.0) * 1024}
+           for k in sorted(set(fk) | set(wk))}
+    rd = sum(v["read_bytes"] for v in per.values())
+    wr = sum(v["write_bytes"] for v in per.values())
+    res = {
+        "op": label, "config": f"n={n}, d={d} (one covariance launch)",
+        "per_kernel": per, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+        "hbm_bytes_per_launch": rd + wr, "algorithmic_bytes_per_launch": 4 * n * d,
+        "correction": "FETCH_SIZE x 1024 x 2 (gfx950 half-count of 16-B/lane reads), WRITE_SIZE x 1024",
+        "caveat": "fabric-side L2 miss counters: Infinity-Cache hits included (upper bound on HBM bytes)",
+        "passes": ["rocprofv3 --pmc FETCH_SIZE --output-format csv -- python3 tools/run_syrk_once.py",
+                   "rocprofv3 --pmc WRITE_SIZE --output-format csv -- python3 tools/run_syrk_once.py"],
+        "source_sha256": source_sha256(),
+    }
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
