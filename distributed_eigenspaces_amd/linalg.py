@@ -28,6 +28,11 @@ __all__ = [
 
 DEFAULT_TOL = 1e-6
 DEFAULT_MAX_SWEEPS = 300
+MAX_K = 128  # the solvers' subspace cap (kMaxP in csrc/capi.hip)
+
+
+class IndefiniteWarning(RuntimeWarning):
+    """topk_eigh returned a negative eigenvalue: the input is not PSD."""
 
 
 @dataclass
@@ -260,7 +265,17 @@ def topk_eigh(S: torch.Tensor, k: int, *, p: int | None = None, tol: float = DEF
     ``eigh(matrix, eigvals=(N-k, N-1))[1]``) that also returns the eigenvalues.
     Only the lower triangle matters mathematically, but the full matrix is read
     (the SYRK output is bit-exactly symmetric).  Raises ValueError for k outside
-    [1, d] like scipy's subset_by_index check.
+    [1, d] like scipy's subset_by_index check, and for k > 128 (the subspace cap).
+
+    S must be symmetric positive semi-definite, as the reference's inputs are
+    (covariances, projector averages, their online sums): subspace iteration
+    finds the largest-magnitude eigenvalues and the Chebyshev filter damps [0, c],
+    so on an indefinite S with |lambda_min| > lambda_k the result can differ from
+    eigh's; a NotConvergedWarning-style ``IndefiniteWarning`` flags a returned
+    eigenvalue below -1e-6 |lambda_max|.  Zero padding (d % 4 != 0, or a subspace
+    wider than d when k is close to d) adds zero eigenvalues: for a rank-deficient
+    S whose top-k reaches into its null space those k-th vectors are arbitrary
+    null-space vectors, as with eigh, but may lie partly in the padding.
     """
     S = require_device_tensor(S, "topk_eigh")
     if S.dim() != 2 or S.shape[0] != S.shape[1]:
@@ -269,9 +284,13 @@ def topk_eigh(S: torch.Tensor, k: int, *, p: int | None = None, tol: float = DEF
     k = int(k)
     if not 1 <= k <= d:
         raise ValueError(f"k={k} out of range [1, {d}]")
+    if k > MAX_K:
+        raise ValueError(f"k={k} > {MAX_K}: the GPU solver's subspace is capped at {MAX_K} columns")
     if check_finite and not bool(torch.isfinite(S).all()):
         raise ValueError("array must not contain infs or NaNs")
     dp = _pad_dim(d)
+    if not p:  # a subspace wider than d (k close to a small d): pad d up to it
+        dp = max(dp, default_subspace(max(dp, (k + 15) // 16 * 16), k))
     if dp != d or S.stride(1) != 1 or S.stride(0) % 4 or S.data_ptr() % 16:
         Sp = torch.zeros((dp, dp), dtype=torch.float32, device=S.device)
         Sp[:d, :d] = S
@@ -295,6 +314,11 @@ def topk_eigh(S: torch.Tensor, k: int, *, p: int | None = None, tol: float = DEF
                                  ctypes.byref(sweeps), ctypes.byref(resid), ws.data_ptr(),
                                  nbytes, _stream(S.device))
     res = _finish(rc, V, evals, sweeps, resid, "deig_topk_sym_f32")
+    ev = res.evals
+    if float(ev[0]) < -1e-6 * float(ev.abs().max()):
+        warnings.warn("topk_eigh: negative eigenvalue returned - the input looks indefinite; the "
+                      "solver assumes a positive semi-definite matrix", IndefiniteWarning,
+                      stacklevel=2)
     if dp != d:
         res.V = res.V[:d].t().contiguous().t()
     return res
@@ -323,7 +347,11 @@ def projavg_topk(Wt: torch.Tensor, k: int, scale: float, *, p: int | None = None
     k = int(k)
     if not 1 <= k <= d:
         raise ValueError(f"k={k} out of range [1, {d}]")
+    if k > MAX_K:
+        raise ValueError(f"k={k} > {MAX_K}: the GPU solver's subspace is capped at {MAX_K} columns")
     dp = _pad_dim(d)
+    if not p:
+        dp = max(dp, default_subspace(max(dp, (k + 15) // 16 * 16), k))
     if dp != d or Wt.stride(1) != 1 or Wt.stride(0) % 4 or Wt.data_ptr() % 16:
         Wp = torch.zeros((mk, dp), dtype=torch.float32, device=Wt.device)
         Wp[:, :d] = Wt

@@ -125,3 +125,35 @@ def test_projavg_rank_deficient_stack(d, k, m, cuda):
     w, V = ref_cpu.server_topk([v.astype(np.float32).astype(np.float64) for v in Vs], k, m)
     assert ref_cpu.projector_distance(r.V.cpu().numpy(), V) <= P_TOL
     np.testing.assert_allclose(r.evals.cpu().numpy(), w, rtol=EV_TOL)
+
+
+@pytest.mark.parametrize("d,k", [(20, 18), (100, 97), (17, 1)])
+def test_k_close_to_small_d(d, k, cuda):
+    """k close to a small d: the subspace is wider than d, so the matrix is padded
+    (r01 raised EINVAL for inputs eigh accepts).  PSD with a clear spectrum."""
+    import distributed_eigenspaces_amd as de
+    lams = np.linspace(3.0, 1.0, d) ** 2
+    S = _matrix(lams, seed=d)
+    r = de.topk_eigh(torch.from_numpy(S).to(cuda), k)
+    assert r.converged and r.V.shape == (d, k)
+    w, V = ref_cpu.top_k_eigh(S.astype(np.float64), k)
+    assert ref_cpu.projector_distance(r.V.cpu().numpy(), V) <= P_TOL
+    np.testing.assert_allclose(r.evals.cpu().numpy(), w, rtol=EV_TOL)
+
+
+def test_indefinite_input_warns(cuda):
+    """The solver assumes PSD (documented); a negative returned eigenvalue warns."""
+    import distributed_eigenspaces_amd as de
+    from distributed_eigenspaces_amd.linalg import IndefiniteWarning
+    d, k = 64, 8
+    lams = np.concatenate([np.linspace(2.0, 1.0, 4), -np.linspace(0.5, 0.1, d - 4)])
+    S = _matrix(lams, seed=9)
+    with pytest.warns(IndefiniteWarning):
+        de.topk_eigh(torch.from_numpy(S).to(cuda), k)
+
+
+def test_k_above_cap_is_a_clear_error(cuda):
+    import distributed_eigenspaces_amd as de
+    S = torch.eye(256, device=cuda)
+    with pytest.raises(ValueError, match="capped at 128"):
+        de.topk_eigh(S, 129)
