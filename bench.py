@@ -18,6 +18,10 @@ line is c3):
   c2  configs[1]: d = 3072, n = 2^20 rows per GPU, k = 16, one worker per GPU;
   c5  configs[4] (stress) per GPU: 8 logical workers x 65,536 rows, d = 16384,
       k = 128 (64 workers on 8 GPUs); server over all workers' bases;
+  c1  configs[0] shape: 50,000 x 3072 uint8 bytes per GPU, 8 logical workers,
+      k = 10, exact int8-MFMA covariance of the bytes (csrc/syrk_u8.hip);
+  c1g the reference's own CIFAR preprocessing: 60,000 x 32x32x3 uint8 pixels,
+      grayscale fused into the covariance (d = 1024), 8 workers, k = 10;
   c4  configs[3] (online): per GPU a stream of 4096 x 3072 batches, Oja steps
       (k = 32), aggregation (all-gather + server solve + broadcast) every 64
       batches; one step = 64 batches + one aggregation.
@@ -33,7 +37,7 @@ samples split into bf16 hi/lo pairs, 3 bf16 MFMA products per fp32 product,
 fp32 accumulation (include/deig.h); "fp32" = the f32 MFMA kernel.  The fp32
 kernel is also timed once outside the timed region (``roofline.fp32_kernel``).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c1|c1g|c4|c5]
        [--syrk-algo auto|split3|fp32]
        (N > 1: either under python -m torch.distributed.run --nproc-per-node N, or
        plain ``python bench.py --gpus N``, which starts the N ranks itself)
@@ -56,6 +60,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 FP32_MFMA_PEAK = 157.3e12  # MI355X_MICROARCH.md: FP32 matrix, dense
 BF16_MFMA_PEAK = 2.5e15    # MI355X_MICROARCH.md: BF16 MFMA, dense (16 x the f32 rate)
+I8_MFMA_PEAK = 5.0e15      # MI355X_MICROARCH.md: I8 MFMA = 2 x BF16 per clock, dense
 HBM_PEAK = 8.0e12
 
 CONFIGS = {
@@ -66,6 +71,12 @@ CONFIGS = {
     "c5": dict(kind="oneshot", rows=8 * 65536, d=16384, k=128, workers=8,
                label="stress: synthetic spiked d=16384 k=128, 8 logical workers x 65536 rows "
                      "per GPU (config 5)"),
+    "c1": dict(kind="oneshot", rows=50000, d=3072, k=10, workers=8, u8="raw",
+               label="configs[0] shape: CIFAR-10 train 50000 x 3072 uint8 bytes (synthetic "
+                     "spiked), 8 threaded workers, k=10, exact int8-MFMA covariance"),
+    "c1g": dict(kind="oneshot", rows=60000, d=1024, k=10, workers=8, u8="gray",
+                label="CIFAR-10 60000 x 32x32x3 uint8 pixels (synthetic spiked) grayscaled "
+                      "in the covariance kernel (distributed.py:170-173), 8 threaded workers, k=10"),
     "c4": dict(kind="oja", rows=4096, d=3072, k=32, agg_every=64, eta=0.02, orth_every=8,
                label="online: Oja mini-batches 4096 x 3072, k=32, aggregation every 64 "
                      "batches (config 4)"),
@@ -141,10 +152,10 @@ def cpu_threaded_oneshot(xs: np.ndarray, n_total: int, k: int, m: int, cores: in
                         else "") + f" -> {t_eig:.1f}s")}
 
 
-def cpu_baseline_oneshot(X_dev: torch.Tensor, n_worker: int, workers: int, k: int,
-                         sample_rows: int, threads: int = 8):
-    """Float64 oracle (oracle/ref_cpu.py) on the first ``sample_rows`` rows of a
-    worker shard, two variants:
+def cpu_baseline_oneshot(xs: np.ndarray, n_worker: int, workers: int, k: int,
+                         threads: int = 8):
+    """Float64 oracle (oracle/ref_cpu.py) on ``xs``, the first rows of a worker
+    shard as the reference's float64 features, two variants:
 
     * m = 1 worker x all BLAS cores: covariance scaled linearly to the full shard
       (it is linear in n), the top-k eigh timed once and counted per worker;
@@ -153,8 +164,7 @@ def cpu_baseline_oneshot(X_dev: torch.Tensor, n_worker: int, workers: int, k: in
 
     ``value`` is the better of the two; both are reported."""
     from oracle import ref_cpu
-    xs = X_dev[:sample_rows].double().cpu().numpy()
-    d = xs.shape[1]
+    sample_rows, d = xs.shape
     cores = int(blas_cores())
     t0 = time.perf_counter()
     S = ref_cpu.sigma_hat(xs)
@@ -356,7 +366,18 @@ def run_oneshot(args, cfg, world, rank, dev):
         n = args.rows
     ni = n // W  # rows per logical worker (distributed.py:99-104 split of the rank block)
     U = synthetic.planted_basis(d, k, seed=0, device=dev)
-    X = synthetic.spiked_samples(n, U, seed=1 + rank)
+    u8 = cfg.get("u8")
+    if u8:
+        # bytes (c1) or interleaved pixels (c1g), resident in HBM like the fp32 shards
+        X = synthetic.spiked_bytes(n, U, seed=1 + rank, channels=3 if u8 == "gray" else 0)
+    else:
+        X = synthetic.spiked_samples(n, U, seed=1 + rank)
+
+    def features(xb):
+        """The reference's float64 sample matrix of a block of X (distributed.py:170-173)."""
+        xb = xb.double()
+        return xb.mean(dim=3).reshape(xb.shape[0], -1) if u8 == "gray" else xb
+
     S = torch.empty((d, d), dtype=torch.float32, device=dev)
     Wt_local = torch.empty((W * k, d), dtype=torch.float32, device=dev)
     # W > 1 logical workers per GPU: each worker's eigensolve runs in its own
@@ -452,9 +473,19 @@ def run_oneshot(args, cfg, world, rank, dev):
     sweeps = [s for _, s in syrk_ev]
     flops = float(ni) * d * (d + 1)  # algorithmic, per worker launch: lower triangle incl. diag
     algo = args.syrk_algo
-    if algo == "auto":
+    if u8:
+        algo = f"u8-{u8}"
+    elif algo == "auto":
         algo = "split3" if ni >= 1024 else "fp32"
-    if algo == "split3":
+    if u8:
+        planes = 3 if u8 == "gray" else 1
+        mfma_flops, peak = planes * flops, I8_MFMA_PEAK
+        kernel = ("covariance u8 (u8_prep_kernel + u8_syrk_kernel v_mfma_i32_16x16x64_i8 + "
+                  "u8_finalize_kernel)")
+        algorithmic = (f"{planes} * n*d*(d+1) = {planes * flops:.4e} int8 MFMA op per launch "
+                       f"(n = {ni} rows" + ("; gray: 3 integer products P_hh, P_ww, P_ll of the "
+                                             "pixel-sum digits" if planes == 3 else "") + ")")
+    elif algo == "split3":
         mfma_flops, peak = 3.0 * flops, BF16_MFMA_PEAK
         kernel = ("covariance split3 (split_kernel + syrks_kernel + syrks_reduce_kernel + "
                   "diag_corr_kernel)")
@@ -465,6 +496,12 @@ def run_oneshot(args, cfg, world, rank, dev):
         kernel = "syrk_kernel (+ syrk_reduce_kernel)"
         algorithmic = f"n*d*(d+1) = {flops:.4e} f32 MFMA flop per launch (n = {ni} rows)"
     achieved = mfma_flops / (syrk_ms * 1e-3)
+    # concurrent workers: the in-loop events also span other workers' solve kernels
+    # interleaved on their side streams, so the covariance is also timed alone
+    syrk_alone_ms = None
+    if concurrent:
+        syrk_alone_ms = time_events(lambda: de.sigma_hat(X[:ni], out=S, algo=args.syrk_algo),
+                                    5, stream)
 
     # --- outside the timed region: accuracy, alternative kernel, sweep roofline
     if concurrent:
@@ -472,7 +509,7 @@ def run_oneshot(args, cfg, world, rank, dev):
         torch.cuda.empty_cache()
     Xw = X[(W - 1) * ni:W * ni]
     cols = torch.randperm(d, generator=torch.Generator().manual_seed(7))[:16].to(dev)
-    Xs = Xw.index_select(1, cols).double()
+    Xs = features(Xw).index_select(1, cols)
     S64 = (Xs.t() @ Xs) / ni
     S_last = Ss[-1] if concurrent else S  # the last worker's covariance
     Sblk = S_last.index_select(0, cols).index_select(1, cols).double()
@@ -492,6 +529,22 @@ def run_oneshot(args, cfg, world, rank, dev):
     p = de.default_subspace(d, k)
     sweep = sweep_roofline(de, S, p, stream)
 
+    acc_u8 = None
+    if u8 and rank == 0:
+        # bytes: the covariance is exact, so the last worker's basis is checked
+        # against float64 eigh of the same shard (the planted U is not the top-k of
+        # an uncentered byte covariance: its mean direction dominates)
+        Xf = features(Xw).cpu()
+        w64, V64 = torch.linalg.eigh(Xf.t() @ Xf / ni)
+        V64 = V64[:, -k:]
+        Vr = r.V.double().cpu()
+        acc_u8 = {"P_dist_last_worker_vs_f64_eigh": float(torch.linalg.matrix_norm(
+                      Vr @ Vr.t() - V64 @ V64.t())),
+                  # both ascending (distributed.py:22-29 order)
+                  "evals_rel_err_vs_f64_eigh": float(((r.evals.double().cpu() - w64[-k:]).abs()
+                                                     / w64[-k:]).max()),
+                  "lambda1_over_lambdak": float(w64[-1] / w64[-k])}
+        del Xf
     if rank != 0:
         return None
     # HBM-side bytes per covariance launch from the separate rocprofv3 PMC passes
@@ -515,18 +568,26 @@ def run_oneshot(args, cfg, world, rank, dev):
             traffic_note = f"unreadable ({e})"
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline_oneshot(X, ni, W, k, min(args.cpu_sample, ni))
-    line = base_line(args, world, elapsed, float(n) * world * args.steps, "f32", {
+        cpu = cpu_baseline_oneshot(features(X[:min(args.cpu_sample, ni)]).cpu().numpy(),
+                                   ni, W, k)
+    line = base_line(args, world, elapsed, float(n) * world * args.steps, "u8" if u8 else "f32", {
         "workload": cfg["label"], "rows_per_gpu": n, "total_rows": n * world, "d": d, "k": k,
         "workers_per_gpu": W, "rows_per_worker": ni, "workers_total": m, "subspace_p": p,
         "parallelism": f"dp{world} ({W} logical worker(s) per GPU, RCCL all-gather of bases)"})
-    line["dtype_note"] = ("fp32 in / fp32 out / fp32 accumulation; split3 covariance and sweeps "
+    if u8:
+        line["data"] = ("synthetic spiked bytes: clip(round(128 + 20 x)) of spiked rows (planted "
+                        "U, theta 8->4)" + ("; 3 channels with independent noise" if u8 == "gray"
+                                            else "") + ", generated on device")
+        line["config"]["image"] = "60000 x 32 x 32 x 3" if u8 == "gray" else None
+    line["dtype_note"] = ("uint8 in, exact int32/int64 integer covariance, fp32 out; eigensolver "
+                          "fp32 with dominant-pair deflation") if u8 else (
+                          "fp32 in / fp32 out / fp32 accumulation; split3 covariance and sweeps "
                           "form each fp32 product from 3 bf16 MFMA products of the split operands "
                           "(hi*hi + hi*lo + lo*hi; covariance restores lo^2 on the diagonal); "
                           "accuracy in accuracy.sigma_hat_rel_err_vs_f64_sampled and the solver "
                           "residuals")
     line["roofline"] = {"bound": "mfma", "kernel": kernel, "achieved": achieved / 1e12,
-                        "peak": peak / 1e12, "unit": "TFLOP/s", "frac": achieved / peak,
+                        "peak": peak / 1e12, "unit": "TOP/s" if u8 else "TFLOP/s", "frac": achieved / peak,
                         "traffic": traffic,
                         "traffic_source": (f"tools/pmc_syrk_{args.config}_{algo}.json (rocprofv3 "
                                            "FETCH_SIZE x2 + WRITE_SIZE, separate passes of this "
@@ -535,6 +596,9 @@ def run_oneshot(args, cfg, world, rank, dev):
                                            f"bytes; {traffic_note})") if traffic else traffic_note,
                         "traffic_vs_algorithmic": (traffic / (4.0 * ni * d)) if traffic else None,
                         "algorithmic": algorithmic, "launch_ms": syrk_ms,
+                        "launch_ms_alone": syrk_alone_ms,
+                        "frac_alone": (mfma_flops / (syrk_alone_ms * 1e-3) / peak
+                                       if syrk_alone_ms else None),
                         # fp32 products per second delivered by the bf16-split kernel:
                         # a throughput, NOT an fp32-MFMA utilisation (the fp32 MFMA
                         # kernel's own utilisation is fp32_kernel.frac)
@@ -550,10 +614,12 @@ def run_oneshot(args, cfg, world, rank, dev):
                          "gather_ms": 1e3 * float(np.mean(rec["gather"])),
                          "server_ms": 1e3 * float(np.mean(rec["server"])),
                          "server_sweeps": res.sweeps}
-    line["accuracy"] = {"sin_theta_server_vs_planted": sin_theta(U, res.V),
-                        "sin_theta_last_worker_vs_planted": sin_theta(U, r.V),
+    line["accuracy"] = {"sin_theta_server_vs_planted": None if u8 else sin_theta(U, res.V),
+                        "sin_theta_last_worker_vs_planted": None if u8 else sin_theta(U, r.V),
                         "worker_resid": r.resid, "server_resid": res.resid,
                         "sigma_hat_rel_err_vs_f64_sampled": sigma_err}
+    if acc_u8:
+        line["accuracy"].update(acc_u8)
     return line
 
 

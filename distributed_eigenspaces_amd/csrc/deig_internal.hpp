@@ -125,8 +125,10 @@ struct RRBuffers {
 };
 int rr_init_launch(float* Z, int64_t d, int p, const float* Q0, int k0, int64_t ldq0,
                    uint64_t seed, hipStream_t stream);
-// max_jsweeps caps the Jacobi sweeps of the small eigenproblem (30 = converge).
-int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream, int max_jsweeps = 30);
+// max_jsweeps caps the Jacobi sweeps of the small eigenproblem (30 = converge);
+// jrel: a pair is rotated while |h_ab| > jrel sqrt(|h_aa h_bb|) (2e-7: to rounding).
+int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream, int max_jsweeps = 30,
+                    float jrel = 2e-7f);
 int rr_update_blocks(int64_t d);
 int rr_power_launch(const RRBuffers& b, int64_t d, int p, float tau, hipStream_t stream);
 // One scaled Chebyshev filter degree on Z = [X_j | A X_j] with T = X_{j-1} (d x p).

@@ -52,22 +52,6 @@ __global__ __launch_bounds__(256) void rr_init_kernel(float* __restrict__ Z, int
   Z[r * 2 * p + j] = v;
 }
 
-__device__ __forceinline__ float block_sum(float v, float* red) {
-  // RT threads -> one value, broadcast.  red has >= RT/64 + 1 floats.
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  __syncthreads();
-  if (l == 0) red[w] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int i = 0; i < RT / 64; ++i) s += red[i];
-    red[RT / 64] = s;
-  }
-  __syncthreads();
-  return red[RT / 64];
-}
-
 // C = A B for p x p row-major matrices in LDS (p % 4 == 0, p <= 128): thread tid
 // owns the 4 x 4 block at (a0, b0) and returns it in acc (false: no block).  Per
 // 4-wide k step: 4 + 4 ds_read_b128 for 64 FMAs into independent accumulators
@@ -100,12 +84,29 @@ __device__ __forceinline__ bool lds_gemm4(const float* A, const float* B, int p,
   return true;
 }
 
-__global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ Cg, int p,
+// Jacobi rotation (c, s) zeroing apq of [[app, apq], [apq, aqq]].  Hardware rcp /
+// sqrt / rsq (~1 ulp): the rotation only has to be orthogonal to rounding
+// (c = rsq(1 + t^2), s = t c), not the exact minimiser, and it sits on the
+// latency chain of every Jacobi step.
+__device__ __forceinline__ void rr_rot_cs(float app, float aqq, float apq, float& c, float& s) {
+  const float tau = (aqq - app) * __builtin_amdgcn_rcpf(2.f * apq);
+  const float t = (fabsf(tau) > 1e18f)
+                      ? 0.5f * __builtin_amdgcn_rcpf(tau)
+                      : copysignf(__builtin_amdgcn_rcpf(
+                                      fabsf(tau) + __builtin_amdgcn_sqrtf(1.f + tau * tau)),
+                                  tau);
+  c = __builtin_amdgcn_rsqf(1.f + t * t);
+  s = t * c;
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void rr_small_kernel(const float* __restrict__ Cg, int p,
                                                       float* __restrict__ Wout,
                                                       float* __restrict__ lam_out,
                                                       float* __restrict__ cs_out,
                                                       float* __restrict__ qs_out,
-                                                      int* __restrict__ info, int max_jsweeps) {
+                                                      int* __restrict__ info, int max_jsweeps,
+                                                      float jrel) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int pp = p * p;
   const int half = p >> 1;
@@ -118,8 +119,8 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
   f32x4* rotp = reinterpret_cast<f32x4*>(gd + p);
   int* rank = reinterpret_cast<int*>(rotp + half);  // p
   float* nq = reinterpret_cast<float*>(rank + p);   // p: ||Q w_j||^2
-  float* red = nq + p;                              // RT/64 + 2
-  int* nrot = reinterpret_cast<int*>(red + RT / 64 + 2);
+  float* red = nq + p;                              // NT/64 + 2
+  int* nrot = reinterpret_cast<int*>(red + NT / 64 + 2);
   const int tid = threadIdx.x;
   const int ldc = 2 * p;
   const float* Mg = Cg;
@@ -132,7 +133,7 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
   };
 
   // ---- 0. D = diag(M)^-1/2;  X1 = D M D
-  for (int a = tid; a < p; a += RT) {
+  for (int a = tid; a < p; a += NT) {
     const float m = Mg[a * ldc + a];
     dsc[a] = (m > 0.f && isfinite(m)) ? rsqrtf(m) : 1.0f;
   }
@@ -142,7 +143,7 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
     info[2] = 0;
   }
   __syncthreads();
-  for (int idx = tid; idx < pp; idx += RT) {
+  for (int idx = tid; idx < pp; idx += NT) {
     const int a = idx / p, b = idx - a * p;
     X1[idx] = Mg[a * ldc + b] * dsc[a] * dsc[b];
   }
@@ -164,9 +165,9 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
   //         recomputes the pivot itself, so one barrier per column.  The pivots
   //         go to gd[] (X1's diagonal still holds D M D's, read by every group)
   //         and onto the diagonal after the loop.
+  constexpr int NG = NT / 8;  // lane groups
   for (int j = 0; j < p; ++j) {
-    const int i = j + grp;
-    if (i < p) {
+    for (int i = j + grp; i < p; i += NG) {
       float sd = 0.f, so = 0.f;
       for (int t = part; t < j; t += 8) {
         const float ljt = X1[j * p + t];
@@ -195,16 +196,15 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
     }
     __syncthreads();
   }
-  for (int a = tid; a < p; a += RT) X1[a * p + a] = gd[a];
-  for (int idx = tid; idx < pp; idx += RT) X2[idx] = 0.f;
+  for (int a = tid; a < p; a += NT) X1[a * p + a] = gd[a];
+  for (int idx = tid; idx < pp; idx += NT) X2[idx] = 0.f;
   __syncthreads();
   stamp(4);
 
   // ---- 2. L^-1 (lower) into X2, row by row; group c owns column c of row i,
   //         its dot over t in [c, i) split over the group's 8 lanes.
   for (int i = 0; i < p; ++i) {
-    const int c = grp;
-    if (c <= i) {
+    for (int c = grp; c <= i; c += NG) {
       float sacc = 0.f;
       for (int t = c + part; t < i; t += 8) sacc = fmaf(X1[i * p + t], X2[t * p + c], sacc);
       sacc = sum8(sacc);
@@ -217,7 +217,7 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
   // ---- 3. X1 = D H D ; 4. T = L^-1 X1, stored transposed (X1 = T^T = X1^T L^-T);
   //         5. X1 = L^-1 X1 = L^-1 H^T L^-T (symmetrised below: the same H~).
   //         Register-blocked 4 x 4 products (lds_gemm4).
-  for (int idx = tid; idx < pp; idx += RT) {
+  for (int idx = tid; idx < pp; idx += NT) {
     const int a = idx / p, b = idx - a * p;
     X1[idx] = Hg[a * ldc + b] * dsc[a] * dsc[b];
   }
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
   }
   // symmetrise H~ and turn X2 = L^-1 into the eigenvector accumulator V0 = L^-T:
   // every Jacobi rotation right-multiplies it, so at the end X2 = L^-T U.
-  for (int idx = tid; idx < pp; idx += RT) {
+  for (int idx = tid; idx < pp; idx += NT) {
     const int a = idx / p, b = idx - a * p;
     if (a < b) {
       const float v = 0.5f * (X1[a * p + b] + X1[b * p + a]);
@@ -266,19 +266,19 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
     nrot[1] = 0;
     nrot[2] = 0;
   }
-  // idx = tid + u RT  ->  (idx / half, idx % half), stepped without divisions
+  // idx = tid + u NT  ->  (idx / half, idx % half), stepped without divisions
   const int tr0 = tid / half, tc0 = tid - tr0 * half;
-  const int dq = RT / half, dr = RT - dq * half;
+  const int dq = NT / half, dr = NT - dq * half;
   for (int sw = 0; sw < max_jsweeps; ++sw) {
     if (tid == 0) nrot[0] = 0;
     // scale for the absolute rotation threshold
     float dmax = 0.f;
-    for (int a = tid; a < p; a += RT) dmax = fmaxf(dmax, fabsf(X1[a * p + a]));
+    for (int a = tid; a < p; a += NT) dmax = fmaxf(dmax, fabsf(X1[a * p + a]));
     for (int o = 32; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o, 64));
     if ((tid & 63) == 0) red[tid >> 6] = dmax;
     __syncthreads();
     float amax = 0.f;
-    for (int i = 0; i < RT / 64; ++i) amax = fmaxf(amax, red[i]);
+    for (int i = 0; i < NT / 64; ++i) amax = fmaxf(amax, red[i]);
     const float abs_thr = 1e-9f * amax;
     // Convergence pre-check (one pass, one barrier): if no pair passes the
     // rotation test now, the first step rotates nothing, the matrix stays as it
@@ -286,12 +286,12 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
     // all-identity sweep that used to end every solve (p - 1 steps, 2 barriers each).
     {
       int need = 0;
-      for (int idx = tid; idx < p * p && !need; idx += RT) {
+      for (int idx = tid; idx < p * p && !need; idx += NT) {
         const int a = idx / p, b = idx - a * p;
         if (b < a) {
           const float apq = X1[a * p + b];
           need = fabsf(apq) > abs_thr &&
-                 fabsf(apq) > 2e-7f * sqrtf(fabsf(X1[a * p + a] * X1[b * p + b]));
+                 fabsf(apq) > jrel * sqrtf(fabsf(X1[a * p + a] * X1[b * p + b]));
         }
       }
       need = __syncthreads_or(need);
@@ -310,13 +310,9 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
         }
         const float app = X1[a * p + a], aqq = X1[b * p + b], apq = X1[a * p + b];
         float c = 1.f, s = 0.f;
-        if (fabsf(apq) > abs_thr && fabsf(apq) > 2e-7f * sqrtf(fabsf(app * aqq))) {
-          const float tau = (aqq - app) / (2.f * apq);
-          const float t = (fabsf(tau) > 1e18f)
-                              ? 0.5f / tau
-                              : copysignf(1.f, tau) / (fabsf(tau) + sqrtf(1.f + tau * tau));
-          c = rsqrtf(1.f + t * t);
-          s = t * c;
+        if (fabsf(apq) > abs_thr &&
+            fabsf(apq) > jrel * __builtin_amdgcn_sqrtf(fabsf(app * aqq))) {
+          rr_rot_cs(app, aqq, apq, c, s);
           atomicAdd(nrot + ci, 1);
         }
         rotp[tid] = f32x4{c, s, __int_as_float(a), __int_as_float(b)};
@@ -325,7 +321,7 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
       const int step_rot = nrot[ci];
       if (step_rot != 0) {  // wave-uniform: identity steps apply nothing
         int tr = tr0, tc = tc0;
-        for (int idx = tid; idx < half * half; idx += RT) {
+        for (int idx = tid; idx < half * half; idx += NT) {
           const f32x4 qr = rotp[tr], qc = rotp[tc];
           const int ar = __float_as_int(qr[2]), br = __float_as_int(qr[3]);
           const int ac = __float_as_int(qc[2]), bc = __float_as_int(qc[3]);
@@ -349,7 +345,7 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
         }
         tr = tr0;
         tc = tc0;
-        for (int idx = tid; idx < p * half; idx += RT) {
+        for (int idx = tid; idx < p * half; idx += NT) {
           const int r = tr, t = tc;
           tr += dq;
           tc += dr;
@@ -383,9 +379,9 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
 
   stamp(7);
   // ---- 7. eigenvalues; W = D (L^-T U)  (row scaling, in place in X2)
-  for (int a = tid; a < p; a += RT) lamv[a] = X1[a * p + a];
+  for (int a = tid; a < p; a += NT) lamv[a] = X1[a * p + a];
   __syncthreads();
-  for (int idx = tid; idx < pp; idx += RT) {
+  for (int idx = tid; idx < pp; idx += NT) {
     const int a = idx / p, b = idx - a * p;
     X2[idx] *= dsc[a];
     X1[idx] = Gg[a * ldc + b];
@@ -405,7 +401,7 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
           X1[(a0 + r) * p + b0 + c] = acc[r][c] * X2[(a0 + r) * p + b0 + c];
     __syncthreads();
   }
-  for (int j = tid; j < p; j += RT) {
+  for (int j = tid; j < p; j += NT) {
     float s = 0.f;
     for (int a = 0; a < p; ++a) s += X1[a * p + j];
     gd[j] = s;
@@ -415,7 +411,7 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
   //         factored exactly, but not for columns whose pivot was floored (a
   //         numerically dependent Q): their Ritz vectors are renormalised by it,
   //         or repeated floored RR steps compound their norms until they overflow.
-  for (int idx = tid; idx < pp; idx += RT) {
+  for (int idx = tid; idx < pp; idx += NT) {
     const int a = idx / p, b = idx - a * p;
     X1[idx] = Mg[a * ldc + b];
   }
@@ -433,7 +429,7 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
           X1[(a0 + r) * p + b0 + c] = acc[r][c] * X2[(a0 + r) * p + b0 + c];
     __syncthreads();
   }
-  for (int j = tid; j < p; j += RT) {
+  for (int j = tid; j < p; j += NT) {
     float s = 0.f;
     for (int a = 0; a < p; ++a) s += X1[a * p + j];
     nq[j] = s;
@@ -453,13 +449,13 @@ __global__ __launch_bounds__(RT) void rr_small_kernel(const float* __restrict__ 
   }
   __syncthreads();
   const float gthr = red[0] * 1e-10f;
-  for (int j = tid; j < p; j += RT) {
+  for (int j = tid; j < p; j += NT) {
     const int rk = rank[j];
     lam_out[rk] = lamv[j];
     cs_out[rk] = (gd[j] > gthr && gd[j] > 0.f) ? rsqrtf(gd[j]) : 0.f;
     qs_out[rk] = (nq[j] > 1e-30f && isfinite(nq[j])) ? rsqrtf(nq[j]) : 1.f;
   }
-  for (int idx = tid; idx < pp; idx += RT) {
+  for (int idx = tid; idx < pp; idx += NT) {
     const int a = idx / p, j = idx - a * p;
     Wout[a * p + rank[j]] = X2[idx];
   }
@@ -669,18 +665,39 @@ int rr_init_launch(float* Z, int64_t d, int p, const float* Q0, int k0, int64_t 
   return DEIG_OK;
 }
 
-int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream, int max_jsweeps) {
+int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream, int max_jsweeps, float jrel) {
   DEIG_REQUIRE(p >= 4 && p <= 128 && p % 4 == 0, "rr_small: p=%d out of range", p);
   const size_t shm = rr_small_shm(p);
   static bool attr = false;
   if (!attr) {
-    DEIG_HIP_CHECK(hipFuncSetAttribute((const void*)rr_small_kernel,
+    DEIG_HIP_CHECK(hipFuncSetAttribute((const void*)rr_small_kernel<RT>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)rr_small_shm(128)));
+    DEIG_HIP_CHECK(hipFuncSetAttribute((const void*)rr_small_kernel<256>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)rr_small_shm(64)));
+    DEIG_HIP_CHECK(hipFuncSetAttribute((const void*)rr_small_kernel<64>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)rr_small_shm(32)));
     attr = true;
   }
-  hipLaunchKernelGGL(rr_small_kernel, dim3(1), dim3(RT), shm, stream, b.C, p, b.W, b.lam, b.cs,
-                     b.qs, b.info, max_jsweeps);
+  // Workgroup size: 1024 threads at every p.  Each Jacobi step is a chain of LDS
+  // round trips per thread, so the most threads (shortest per-thread chain) win:
+  // measured r02 at p = 32, Jacobi 75 us (1024) vs 89 (256) vs 184 (64) per RR.
+  // DEIG_RR_THREADS=64|256 selects the narrower builds for such comparisons.
+  static const int nt_env = getenv("DEIG_RR_THREADS") ? atoi(getenv("DEIG_RR_THREADS")) : 0;
+  int nt = RT;
+  if (nt_env == 64 && p <= 32) nt = 64;
+  if (nt_env == 256 && p <= 64) nt = 256;
+  if (nt == 64)
+    hipLaunchKernelGGL(rr_small_kernel<64>, dim3(1), dim3(64), shm, stream, b.C, p, b.W, b.lam,
+                       b.cs, b.qs, b.info, max_jsweeps, jrel);
+  else if (nt == 256)
+    hipLaunchKernelGGL(rr_small_kernel<256>, dim3(1), dim3(256), shm, stream, b.C, p, b.W, b.lam,
+                       b.cs, b.qs, b.info, max_jsweeps, jrel);
+  else
+    hipLaunchKernelGGL(rr_small_kernel<RT>, dim3(1), dim3(RT), shm, stream, b.C, p, b.W, b.lam,
+                       b.cs, b.qs, b.info, max_jsweeps, jrel);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }

@@ -13,7 +13,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-__all__ = ["planted_basis", "spiked_theta", "spiked_samples"]
+__all__ = ["planted_basis", "spiked_theta", "spiked_samples", "spiked_bytes"]
 
 
 def planted_basis(d: int, k: int, seed: int = 0, device=None) -> torch.Tensor:
@@ -45,3 +45,28 @@ def spiked_samples(n: int, U: torch.Tensor, seed: int = 1, theta_hi: float = 8.0
         h = torch.randn((hi - lo, k), generator=gen, device=dev, dtype=torch.float32)
         blk.addmm_(h, Ut)
     return X
+
+
+def spiked_bytes(n: int, U: torch.Tensor, seed: int = 1, scale: float = 20.0,
+                 channels: int = 0) -> torch.Tensor:
+    """CIFAR-like uint8 samples on U's device: clip(round(128 + scale * x)) of
+    spiked_samples rows x (CIFAR is not shipped with the reference).
+
+    channels = 0: (n, d) raw bytes.  channels = 3: (n, H, W, 3) interleaved pixels
+    (load_data.py:18-33 layout, H = W = sqrt(d)) whose channel c is x plus
+    independent N(0, 1/4) noise, so the reference's grayscale (distributed.py:171)
+    keeps U as the planted subspace.  The uncentered covariance of such bytes has
+    the mean direction as its dominant eigenvector, as CIFAR's does."""
+    d = U.shape[0]
+    xf = spiked_samples(n, U, seed)
+    if not channels:
+        return xf.mul_(scale).add_(128.0).round_().clamp_(0, 255).to(torch.uint8)
+    side = int(round(d ** 0.5))
+    if side * side != d:
+        raise ValueError(f"spiked_bytes: d = {d} is not a square image")
+    out = torch.empty((n, d, channels), dtype=torch.uint8, device=U.device)
+    gen = torch.Generator(device=U.device).manual_seed(int(seed) * 7919 + 17)
+    for c in range(channels):
+        noise = torch.randn((n, d), generator=gen, device=U.device, dtype=torch.float32)
+        out[:, :, c] = noise.mul_(0.5).add_(xf).mul_(scale).add_(128.0).round_().clamp_(0, 255)
+    return out.view(n, side, side, channels)
