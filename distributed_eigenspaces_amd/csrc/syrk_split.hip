@@ -70,7 +70,27 @@ struct SSched {
   int beta;
   int flush_kt;  // K-tiles between two-level flushes of the accumulators
   int prio;      // 1: waves 4-7 run at s_setprio 1 (the arbitration losers otherwise)
+  unsigned* pace;  // per-XCD arrival counters (128 B apart), zeroed per launch
+  int pace_kt;     // K-tiles between two XCD pacing points (0: off)
 };
+
+// XCD pacing point of the full-tile phases: the ~G/8 blocks on one XCD run
+// neighbouring tiles of one super-tile and read the same K rows of its panels, but
+// drift apart over ~10^5 K-tiles until their shared panels no longer meet in the
+// XCD's 4 MB L2.  Every pace_kt K-tiles one lane per block adds 1 to its XCD's
+// counter and waits (bounded: 20 us of s_memrealtime, so a block that is not
+// resident can only cost time, never a hang) until all of the XCD's blocks have
+// arrived.  Relaxed atomics, no fence: nothing is published, so no L2 write-back.
+// The result's wait (vmcnt(0)) also drains this wave's ring DMAs, which keeps the
+// counted vmcnt waits exact.
+__device__ __noinline__ void xcd_pace(unsigned* ctr, unsigned target) {
+  __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    if (wall_clock64() - t0 > 2000) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
 
 
 __device__ __forceinline__ i32x4 make_rsrc(const void* base, uint32_t nrec) {
@@ -347,7 +367,7 @@ __device__ __forceinline__ void store4(const SSched& s, int ib, int j, bool diag
 
 template <int MF, int KT, int NST>
 __device__ __forceinline__ void segment(const SSched& s, unsigned char* lds, int tile, int64_t k0, int64_t k1,
-                        int slot, bool partial) {
+                        int slot, bool partial, int pace_j) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wi = wave >> 2, wj = wave & 3;
@@ -373,9 +393,17 @@ __device__ __forceinline__ void segment(const SSched& s, unsigned char* lds, int
     constexpr int BUF_B = Geo<KT>::BUF_B;
     for (int t = 0; t < NST - 1 && t < nkt; ++t)
       stage<KT>(s, k0 + t, i0, j0, diag, lds + t * BUF_B, wave, lane16);
-    int cur = 0, nxt = NST - 1, since = 0;
+    int cur = 0, nxt = NST - 1, since = 0, since_pace = 0;
+    // pacing target: blocks on this XCD x arrival index
+    const int xcd = blockIdx.x & 7;
+    const unsigned nx = (unsigned)((s.G >> 3) + (xcd < (s.G & 7) ? 1 : 0));
     for (int64_t t = 0; t < nkt; ++t) {
       const int64_t left = nkt - 1 - t;
+      if (pace_j >= 0 && ++since_pace == s.pace_kt) {
+        since_pace = 0;
+        ++pace_j;
+        if (threadIdx.x == 0) xcd_pace(s.pace + 32 * xcd, (unsigned)pace_j * nx);
+      }
       // RAW: this wave's DMAs of stage t landed (counted vmcnt), then a barrier
       // every reader passes.  WAR: stage t-1's ds_reads retired (lgkmcnt) before
       // the barrier, so its buffer can be restaged right after it.  A raw
@@ -444,7 +472,9 @@ __global__ __launch_bounds__(NTHR) void syrks_kernel(SSched s) {
       k0 = __builtin_amdgcn_readfirstlane((int)(s.NK * sg / s.nseg));
       k1 = __builtin_amdgcn_readfirstlane((int)(s.NK * (sg + 1) / s.nseg));
     }
-    segment<MF, KT, NST>(s, lds, tile, k0, k1, slot, partial);
+    // full phases pace (identical K work on every block); remainder items do not
+    const int pace_j = (!partial && s.pace_kt > 0) ? (int)(w * (s.NK / s.pace_kt)) : -1;
+    segment<MF, KT, NST>(s, lds, tile, k0, k1, slot, partial, pace_j);
   }
 }
 
@@ -562,7 +592,7 @@ int remainder_segments(int64_t R, int G) {
 
 struct Layout {
   int64_t dp, nt, T, G, q, R, nseg, yb_max, chunk_rows;
-  size_t off_order, off_accs, off_part, off_corr, off_xp, total;
+  size_t off_order, off_pace, off_accs, off_part, off_corr, off_xp, total;
 };
 
 // Workspace: [order][G flush slabs][R * nseg remainder slabs][corr YB x dp][XP chunk].
@@ -580,6 +610,8 @@ Layout make_layout(int64_t n, int64_t d, int G, int64_t chunk_rows) {
   size_t off = 0;
   L.off_order = off;
   off = align_up(off + sizeof(int) * L.T, 256);
+  L.off_pace = off;
+  off += 8 * 128;  // 8 XCD counters, one per 128-B line
   L.off_accs = off;
   off += sizeof(float) * (size_t)G * SLAB;
   L.off_part = off;
@@ -660,6 +692,13 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
   if (flush_rows > (int64_t(1) << 30)) flush_rows = int64_t(1) << 30;
   s.prio = 0;
   if (const char* v = getenv("DEIG_SYRK_PRIO")) s.prio = atoi(v);
+  s.pace = reinterpret_cast<unsigned*>(base + L.off_pace);
+  // XCD pacing every 64 K-tiles (2048 rows): config 3 L2 hit rate 0.52 -> 0.75, fabric
+  // read requests halved, 345 -> 334 ms (r02, interleaved A/B in one process;
+  // 16 / 32 / 128 / 256 K-tiles measured 0.3-1.5 % slower).  DEIG_SYRK_PACE=0: off.
+  s.pace_kt = 64;
+  if (const char* v = getenv("DEIG_SYRK_PACE")) s.pace_kt = atoi(v);
+  if (s.pace_kt < 0) s.pace_kt = 0;
   hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(64), 0, stream, s.nt,
                      reinterpret_cast<int*>(base + L.off_order));
   DEIG_HIP_CHECK(hipGetLastError());
@@ -679,6 +718,7 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
     s.beta = c > 0 ? 1 : 0;
     s.flush_kt = (int)(flush_rows / (16 * kt_steps));
     const bool mf16 = variant >= 100;
+    if (s.pace_kt > 0) DEIG_HIP_CHECK(hipMemsetAsync(s.pace, 0, 8 * 128, stream));
     switch (variant) {
       case 13: hipLaunchKernelGGL((syrks_kernel<32, 1, 3>), dim3(G), dim3(NTHR), 0, stream, s); break;
       case 14: hipLaunchKernelGGL((syrks_kernel<32, 1, 4>), dim3(G), dim3(NTHR), 0, stream, s); break;

@@ -1,7 +1,7 @@
 """A/B split3 SYRK settings in one process on the config-3 shard.
 
 Each setting is "variant[:ENV=value,...]" where variant is DEIG_SYRK_VARIANT and
-the extra pairs are DEIG_SYRK_<ENV> overrides (FLUSH_ROWS, PRIO).  Also reports
+the extra pairs are DEIG_SYRK_<ENV> overrides (FLUSH_ROWS, PRIO, PACE).  Also reports
 whether each setting reproduces the first setting's Sigma_hat bit for bit (same
 accumulation order -> identical; a cheap race screen) and its max deviation.
 
@@ -18,7 +18,7 @@ from distributed_eigenspaces_amd import synthetic  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else (1 << 21)
 d = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
 settings = sys.argv[3:] or ["162", "22"]
-KEYS = ("DEIG_SYRK_VARIANT", "DEIG_SYRK_FLUSH_ROWS", "DEIG_SYRK_PRIO")
+KEYS = ("DEIG_SYRK_VARIANT", "DEIG_SYRK_FLUSH_ROWS", "DEIG_SYRK_PRIO", "DEIG_SYRK_PACE")
 
 
 def apply(setting):
