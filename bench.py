@@ -242,29 +242,33 @@ def sweep_roofline(de, S: torch.Tensor, p: int, stream) -> dict:
     byt, fl = 4.0 * d * d, 2.0 * d * d * p
     out = {"d": d, "p": p, "bound": "hbm", "algorithmic": "4 d^2 bytes (S read once), 2 d^2 p flop",
            "peak_GBs": HBM_PEAK / 1e9}
-    for algo in ("bf16x5", "bf16x6", "fp32"):
+    for algo in ("bf16x3", "bf16x5", "bf16x6", "fp32"):
         if algo != "fp32":
-            # as in the solver: the S image is built once per solve (timed apart),
-            # then every sweep streams it; bf16x5 = the solver's mode (Q rounded in
-            # place to two bf16 pieces, five products; Q' is idempotent under it)
-            rq = algo == "bf16x5"
-            prep_ms = time_events(lambda: de.sym_apply(S, Q, out=Y, round_q=rq), 5, stream)
-            ms = time_events(lambda: de.sym_apply(S, Q, out=Y, prepared=True, round_q=rq), 20,
-                             stream)
+            # as in the solver: the S images are built once per solve (timed apart),
+            # then every sweep streams one; bf16x3 / bf16x5 = the solver's modes (Q
+            # rounded in place to two bf16 pieces, idempotent; bf16x3 also reads S as
+            # two pieces from the prepared two-piece image: three products)
+            rq, fa = algo in ("bf16x3", "bf16x5"), algo == "bf16x3"
+            prep_ms = time_events(lambda: de.sym_apply(S, Q, out=Y, round_q=rq, fast=fa), 5,
+                                  stream)
+            ms = time_events(lambda: de.sym_apply(S, Q, out=Y, prepared=True, round_q=rq,
+                                                  fast=fa), 20, stream)
         else:
             ms = time_events(lambda: de.sym_apply(S, Q, algo=algo, out=Y), 20, stream)
         t = ms * 1e-3
-        nprod = {"bf16x5": 5, "bf16x6": 6}.get(algo)
+        nprod = {"bf16x3": 3, "bf16x5": 5, "bf16x6": 6}.get(algo)
         t_min = max(byt / HBM_PEAK, fl / (BF16_MFMA_PEAK / nprod if nprod else FP32_MFMA_PEAK))
         out[algo] = {"us": ms * 1e3, "hbm_GBs": byt / t / 1e9, "hbm_frac": byt / t / HBM_PEAK,
                      "fp32_equiv_tflops": fl / t / 1e12, "attainable_frac": t_min / t}
         if nprod:
             out[algo]["image_prepare_us_once_per_solve"] = max(prep_ms - ms, 0.0) * 1e3
-    out["kernel"] = ("bf16x5 (solver) / bf16x6 (exact Q): split_q_kernel + sweep2_kernel (p <= 80) / "
-                     "sweep3_kernel (p > 80) (+ sweep_reduce_kernel) on the S image "
-                     "(sweep_prepare_kernel, once per solve), 5 / 6 bf16 MFMA 16x16x32 products of "
-                     "3-piece split S rows and 2- / 3-piece Q; fp32: skinny_kernel<T> f32 MFMA 16x16x4")
-    out["solver_uses"] = "bf16x5"
+    out["kernel"] = ("split_q_kernel + sweep2_kernel (p <= 80) / sweep3_kernel (p > 80) (+ "
+                     "sweep_reduce_kernel) on the S images (sweep_prepare_kernel, once per solve): "
+                     "bf16x3 = 3 bf16 MFMA 16x16x32 products of the prepared two-piece S image and "
+                     "two-piece Q; bf16x5 / bf16x6 = 5 / 6 products of S rows split into 3 pieces "
+                     "in registers and 2- / 3-piece Q; fp32: skinny_kernel<T> f32 MFMA 16x16x4")
+    out["solver_uses"] = ("bf16x3 while the residual is above 1e-3, bf16x5 down to 1e-4, "
+                          "bf16x6 below")
     return out
 
 

@@ -134,14 +134,14 @@ SolverWs carve_solver(void* ws, size_t cap, int64_t d, int k, int p, int64_t mk,
 }
 
 int apply_op(const Operator& op, const SolverWs& w, int64_t d, int p, hipStream_t st,
-             bool round_q) {
+             int smode) {
   float* Q = w.rr.Z;
   float* Y = w.rr.Z + p;
   const int64_t ld = 2 * p;
   if (!op.implicit) {
     if (w.sweep_ws)
       return sweep_apply(op.S, d, op.lds, Q, p, ld, Y, ld, 1.f, w.sweep_ws, w.sweep_bytes, st,
-                         round_q);
+                         smode);
     return skinny_launch(true, op.S, op.lds, Q, ld, Y, ld, d, p, d, 1.f, 0.f, w.slab,
                          w.slab_bytes, st);
   }
@@ -251,6 +251,11 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
       getenv("DEIG_JACOBI_EARLY") ? atoi(getenv("DEIG_JACOBI_EARLY")) : 3;
   static const float jcap_above =
       getenv("DEIG_JACOBI_EARLY_ABOVE") ? (float)atof(getenv("DEIG_JACOBI_EARLY_ABOVE")) : 1e-2f;
+  // Early sweeps (residual above fast_until) take S as its two leading bf16 pieces
+  // too: three products, no split in the sweep, ~2^-16 relative - 100x below the
+  // residual there (sweep.hip sweep_products SP = 2).  DEIG_SWEEP_FAST_UNTIL=0: off.
+  static const float fast_until =
+      getenv("DEIG_SWEEP_FAST_UNTIL") ? (float)atof(getenv("DEIG_SWEEP_FAST_UNTIL")) : 1e-3f;
   static const float round_until =
       getenv("DEIG_SWEEP_ROUND_UNTIL") ? (float)atof(getenv("DEIG_SWEEP_ROUND_UNTIL")) : 1e-4f;
 
@@ -263,7 +268,9 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
     last = 3.4e38f;
     converged = false;
     while (it < max_sweeps) {
-      const bool round_q = last > fmaxf(round_until, tol);
+      const int smode = (fast_until > 0.f && last > fmaxf(fast_until, tol)) ? kSweepFast
+                        : last > fmaxf(round_until, tol)                 ? kSweepRoundQ
+                                                                         : kSweepExact;
       ChebPlan plan;
       const bool cheb = cheb_on && nrr > 0 && cheb_plan(lam_h, kc, p, last, tol, &plan);
       int ncheb = 0, rc2;
@@ -272,7 +279,7 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
         const int m = std::min(plan.m, max_sweeps - it - 1);
         double s_prev = plan.s1;
         for (int j = 0; j < m; ++j, ++it) {
-          if ((rc2 = apply_op(op, w, d, p, st, round_q))) return rc2;
+          if ((rc2 = apply_op(op, w, d, p, st, smode))) return rc2;
           double alpha, gamma;
           if (j == 0) {
             alpha = plan.s1 / plan.e;
@@ -291,12 +298,12 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
       } else if (nrr > 0) {
         const int npow = std::min(rr_every - 1, max_sweeps - it - 1);
         for (int j = 0; j < npow; ++j, ++it) {
-          if ((rc2 = apply_op(op, w, d, p, st, round_q))) return rc2;
+          if ((rc2 = apply_op(op, w, d, p, st, smode))) return rc2;
           // power step on the live Ritz columns of the last RR (Q_j <- Y_j / ||Y w_j||)
           if ((rc2 = rr_power_launch(w.rr, d, p, tau, st))) return rc2;
         }
       }
-      if ((rc2 = apply_op(op, w, d, p, st, round_q))) return rc2;
+      if ((rc2 = apply_op(op, w, d, p, st, smode))) return rc2;
       ++it;
       if ((rc2 = skinny_launch(true, w.rr.Z, 2 * p, w.rr.Z, 2 * p, w.rr.C, 2 * p, 2 * p, 2 * p,
                                d, 1.f, 0.f, w.slab, w.slab_bytes, st)))
@@ -504,7 +511,7 @@ int deig_projavg_topk_f32(const float* Wt, int64_t d, int64_t mk, int64_t ldw, f
 }
 
 size_t deig_sym_apply_workspace(int64_t d, int p, int algo) {
-  algo &= ~(DEIG_SWEEP_PREPARED | DEIG_SWEEP_ROUND_Q);
+  algo &= ~(DEIG_SWEEP_PREPARED | DEIG_SWEEP_ROUND_Q | DEIG_SWEEP_FAST);
   if (algo == DEIG_SWEEP_FP32) return skinny_workspace_bytes(d, p, d);
   return sweep_workspace_bytes(d, p);
 }
@@ -517,8 +524,10 @@ int deig_sym_apply_f32(const float* S, int64_t d, int64_t lds, const float* Q, i
     return skinny_launch(true, S, lds, Q, ldq, Y, ldy, d, p, d, alpha, 0.f,
                          static_cast<float*>(ws), ws_bytes, (hipStream_t)stream);
   const bool prepared = (algo & DEIG_SWEEP_PREPARED) != 0;
-  const bool round_q = (algo & DEIG_SWEEP_ROUND_Q) != 0;
-  algo &= ~(DEIG_SWEEP_PREPARED | DEIG_SWEEP_ROUND_Q);
+  const int smode = (algo & DEIG_SWEEP_FAST)      ? kSweepFast
+                    : (algo & DEIG_SWEEP_ROUND_Q) ? kSweepRoundQ
+                                                  : kSweepExact;
+  algo &= ~(DEIG_SWEEP_PREPARED | DEIG_SWEEP_ROUND_Q | DEIG_SWEEP_FAST);
   if (algo != DEIG_SWEEP_AUTO && algo != DEIG_SWEEP_BF16X6)
     return fail(DEIG_EINVAL, "sym_apply: unknown algorithm %d", algo);
   if (!prepared) {
@@ -526,7 +535,7 @@ int deig_sym_apply_f32(const float* S, int64_t d, int64_t lds, const float* Q, i
     if (rc) return rc;
   }
   return sweep_apply(S, d, lds, Q, p, ldq, Y, ldy, alpha, ws, ws_bytes, (hipStream_t)stream,
-                     round_q);
+                     smode);
 }
 
 size_t deig_oja_workspace(int64_t b, int64_t d, int k) { return oja_workspace_bytes(b, d, k); }

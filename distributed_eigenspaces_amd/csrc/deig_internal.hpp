@@ -102,12 +102,16 @@ int sweep_prepare(const float* S, int64_t d, int64_t lds, int p, void* ws, size_
                   const float* lamd = nullptr, int r = 0);
 // 1 = the row-major v1 sweep (reads S in place, no image, no deflation).
 int sweep_version();
-// round_q: the solver's in-place mode - Q (which must then be writable) is
-// rounded to 16 significant bits (Q' = h + m, two bf16 pieces) and the product
-// S Q' formed with five bf16 products instead of six (sweep.hip split_q_kernel).
+// mode 0: exact (six products).  mode 1 (round_q): the solver's in-place mode - Q
+// (which must then be writable) is rounded to 16 significant bits (Q' = h + m, two
+// bf16 pieces) and the product S Q' formed with five bf16 products instead of six
+// (sweep.hip split_q_kernel).  mode 2 (early sweeps): as 1, and S is taken as its
+// two leading bf16 pieces from the prepared two-piece image - three products, no
+// split in the sweep, ~2^-16 relative.
+constexpr int kSweepExact = 0, kSweepRoundQ = 1, kSweepFast = 2;
 int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
                 float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st,
-                bool round_q = false);
+                int mode = kSweepExact);
 
 // Rayleigh-Ritz pieces (rr.hip).
 struct RRBuffers {

@@ -280,12 +280,24 @@ __global__ __launch_bounds__(SW_THR) void sweep_kernel(const float* __restrict__
 // The products of one Q fragment (pieces bh, bm[, bl]) with MB split S
 // fragments into column block j, small terms first, MB independent accumulators
 // between dependent MFMAs.  NP = 3: hh + hm + mh + hl + lh + mm (six); NP = 2
-// (Q = bh + bm exactly): hh + hm + mh + mm + lh (five; bl unused).
-template <int MB, int NP, int NB>
+// (Q = bh + bm exactly): hh + hm + mh + mm + lh (five; bl unused).  SP = 2 (the
+// early-sweep mode: S taken as its two leading pieces, Q two pieces): hh + hm + mh
+// (three; al, bl unused; dropped m m ~2^-18, S's own rounding 2^-17).
+template <int MB, int NP, int SP, int NB>
 __device__ __forceinline__ void sweep_products(f32x4 (&acc)[MB][NB], int j, const u32x4 (&ah)[MB],
                                                const u32x4 (&am)[MB], const u32x4 (&al)[MB],
                                                const u32x4& bh, const u32x4& bm,
                                                const u32x4& bl) {
+  if constexpr (SP == 2) {
+    static_assert(NP == 2, "two-piece S pairs with two-piece Q");
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bm, acc[mb][j]);
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(am[mb], bh, acc[mb][j]);
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bh, acc[mb][j]);
+    return;
+  }
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(am[mb], bm, acc[mb][j]);
   if constexpr (NP == 3) {
@@ -331,6 +343,7 @@ __global__ __launch_bounds__(256) void sweep_prepare_kernel(const float* __restr
                                                             int64_t lds, int64_t d, int64_t ng,
                                                             int64_t nunits,
                                                             f32x4* __restrict__ SI,
+                                                            u32x4* __restrict__ SH,
                                                             const float* __restrict__ Vd,
                                                             int64_t ldv,
                                                             const float* __restrict__ lamd,
@@ -369,6 +382,13 @@ __global__ __launch_bounds__(256) void sweep_prepare_kernel(const float* __restr
   f32x4* dst = SI + ((t * 4 + mb) * 2) * 64 + lane;
   dst[0] = v0;
   dst[64] = v1;
+  // two-piece image (same addressing): the h and m pieces of these 8 values, the
+  // early sweeps' operand - read as is, no split in the sweep
+  u32x4 h, m, l;
+  split8(v0, v1, h, m, l);
+  u32x4* dh = SH + ((t * 4 + mb) * 2) * 64 + lane;
+  dh[0] = h;
+  dh[64] = m;
 }
 
 // Sweep kernel v2: independent waves, no LDS, no barriers.
@@ -384,7 +404,9 @@ __global__ __launch_bounds__(256) void sweep_prepare_kernel(const float* __restr
 // independently, each with a D-deep register ring of S and Q fragments.
 // PROBE (diagnostic builds only, DEIG_SWEEP_PROBE): bit 0 drops the MFMAs, bit 1
 // the S loads, bit 2 the Q loads (results are then garbage).
-template <int NB, int NP, int PROBE = 0>
+// PRE: SI is the two-piece image (sweep_prepare_kernel's SH: h | m per half slot)
+// and the products are the three of SP = 2 - the early-sweep mode, no split.
+template <int NB, int NP, int PROBE = 0, bool PRE = false>
 __global__ __launch_bounds__(256, 1) void sweep2_kernel(const f32x4* __restrict__ SI, int64_t d,
                                                         const u32x4* __restrict__ QS,
                                                         int64_t ngrp, float* __restrict__ Y,
@@ -443,8 +465,15 @@ __global__ __launch_bounds__(256, 1) void sweep2_kernel(const f32x4* __restrict_
   };
   auto split_into = [&](int ps, int b) {
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb)
-      split8(sr[b][mb][0], sr[b][mb][1], pc[ps][0][mb], pc[ps][1][mb], pc[ps][2][mb]);
+    for (int mb = 0; mb < MB; ++mb) {
+      if constexpr (PRE) {
+        pc[ps][0][mb] = __builtin_bit_cast(u32x4, sr[b][mb][0]);
+        pc[ps][1][mb] = __builtin_bit_cast(u32x4, sr[b][mb][1]);
+        pc[ps][2][mb] = pc[ps][1][mb];  // unused by the SP = 2 products
+      } else {
+        split8(sr[b][mb][0], sr[b][mb][1], pc[ps][0][mb], pc[ps][1][mb], pc[ps][2][mb]);
+      }
+    }
   };
   // Body of group g: S slot of g + 1 is SB1 = (g + 1) % 3, Q slot / piece set
   // QB = g & 1.  The tail loads and splits clamped copies of the last group.
@@ -463,7 +492,7 @@ __global__ __launch_bounds__(256, 1) void sweep2_kernel(const f32x4* __restrict_
           acc[mb][j][0] += __uint_as_float((ah[mb][0] ^ am[mb][1] ^ al[mb][2] ^ bh[0] ^ bm[1] ^ bl[2]) & 0x3fffffffu);
         continue;
       }
-      sweep_products<MB, NP>(acc, j, ah, am, al, bh, bm, bl);
+      sweep_products<MB, NP, PRE ? 2 : 3>(acc, j, ah, am, al, bh, bm, bl);
     }
     load_q(QB, g + 2);   // the Q slot just consumed
     load_s(SB1, g + 4);  // the S slot just split
@@ -539,7 +568,7 @@ __device__ __forceinline__ void sw_dma16(const __amdgpu_buffer_rsrc_t rsrc, int 
                : "memory", "m0");
 }
 
-template <int NB, int NP, int D, int OCC = 1>
+template <int NB, int NP, int D, int OCC = 1, bool PRE = false>
 __global__ __launch_bounds__(256, OCC) void sweep3_kernel(const f32x4* __restrict__ SI, int64_t d,
                                                         const u32x4* __restrict__ QS,
                                                         int64_t ngrp, float* __restrict__ Y,
@@ -598,13 +627,21 @@ __global__ __launch_bounds__(256, OCC) void sweep3_kernel(const f32x4* __restric
     asm volatile("" ::: "memory");
     u32x4 ah[MB], am[MB], al[MB];
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) split8(sr[B][mb][0], sr[B][mb][1], ah[mb], am[mb], al[mb]);
+    for (int mb = 0; mb < MB; ++mb) {
+      if constexpr (PRE) {
+        ah[mb] = __builtin_bit_cast(u32x4, sr[B][mb][0]);
+        am[mb] = __builtin_bit_cast(u32x4, sr[B][mb][1]);
+        al[mb] = am[mb];  // unused by the SP = 2 products
+      } else {
+        split8(sr[B][mb][0], sr[B][mb][1], ah[mb], am[mb], al[mb]);
+      }
+    }
     const u32x4* qs = reinterpret_cast<const u32x4*>(qlds + (int)(g % NS) * SLOT) + lane;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const u32x4 bh = qs[(j * NP + 0) * 64], bm = qs[(j * NP + 1) * 64];
       const u32x4 bl = qs[(j * NP + NP - 1) * 64];
-      sweep_products<MB, NP>(acc, j, ah, am, al, bh, bm, bl);
+      sweep_products<MB, NP, PRE ? 2 : 3>(acc, j, ah, am, al, bh, bm, bl);
     }
     // Refill D groups ahead (clamped: the tail re-loads the last group into its
     // own slot, which holds the same bytes, so no reader sees a change).
@@ -711,10 +748,15 @@ void launch_v1(dim3 grid, hipStream_t st, const float* S, int64_t lds, int64_t d
                      Y, ldy, alpha, part);
 }
 
-template <int NB, int NP>
+template <int NB, int NP, bool PRE>
 void launch_v2(dim3 grid, hipStream_t st, const f32x4* SI, int64_t d, const u32x4* QS, float* Y,
                int64_t ldy, float alpha, float* part) {
   const int64_t ng = si_groups(d);
+  if constexpr (PRE) {
+    hipLaunchKernelGGL((sweep2_kernel<NB, NP, 0, true>), grid, dim3(256), 0, st, SI, d, QS, ng, Y,
+                       ldy, alpha, part);
+    return;
+  }
   if constexpr (NB == 5 && NP == 3) {
     static const int probe = getenv("DEIG_SWEEP_PROBE") ? atoi(getenv("DEIG_SWEEP_PROBE")) : 0;
     switch (probe) {
@@ -733,32 +775,33 @@ void launch_v2(dim3 grid, hipStream_t st, const f32x4* SI, int64_t d, const u32x
                      alpha, part);
 }
 
-template <int NB, int NP>
+template <int NB, int NP, bool PRE>
 void launch_v3(dim3 grid, hipStream_t st, const f32x4* SI, int64_t d, const u32x4* QS, float* Y,
                int64_t ldy, float alpha, float* part) {
   static const int de = getenv("DEIG_SWEEP_DEPTH") ? atoi(getenv("DEIG_SWEEP_DEPTH")) : 3;
   const int64_t ng = si_groups(d);
   if (de == 4)
-    hipLaunchKernelGGL((sweep3_kernel<NB, NP, 4>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy,
-                       alpha, part);
+    hipLaunchKernelGGL((sweep3_kernel<NB, NP, 4, 1, PRE>), grid, dim3(256), 0, st, SI, d, QS, ng,
+                       Y, ldy, alpha, part);
   else if (de == 2)
-    hipLaunchKernelGGL((sweep3_kernel<NB, NP, 2>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy,
-                       alpha, part);
+    hipLaunchKernelGGL((sweep3_kernel<NB, NP, 2, 1, PRE>), grid, dim3(256), 0, st, SI, d, QS, ng,
+                       Y, ldy, alpha, part);
   else
-    hipLaunchKernelGGL((sweep3_kernel<NB, NP, 3>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy,
-                       alpha, part);
+    hipLaunchKernelGGL((sweep3_kernel<NB, NP, 3, 1, PRE>), grid, dim3(256), 0, st, SI, d, QS, ng,
+                       Y, ldy, alpha, part);
 }
 
-// v2 (sweep3 = false) or v3 with NP Q pieces, NB = p / 16 column blocks.
-template <int NP>
+// v2 (sweep3 = false) or v3 with NP Q pieces, NB = p / 16 column blocks; PRE: the
+// two-piece S image (three products).
+template <int NP, bool PRE = false>
 void launch_image(bool v3, int nb, dim3 grid, hipStream_t st, const f32x4* SI, int64_t d,
                   const u32x4* QS, float* Y, int64_t ldy, float alpha, float* part) {
-#define DEIG_NB_CASE(N_)                                              \
-  case N_:                                                            \
-    if (v3)                                                           \
-      launch_v3<N_, NP>(grid, st, SI, d, QS, Y, ldy, alpha, part);    \
-    else                                                              \
-      launch_v2<N_, NP>(grid, st, SI, d, QS, Y, ldy, alpha, part);    \
+#define DEIG_NB_CASE(N_)                                                   \
+  case N_:                                                                 \
+    if (v3)                                                                \
+      launch_v3<N_, NP, PRE>(grid, st, SI, d, QS, Y, ldy, alpha, part);    \
+    else                                                                   \
+      launch_v2<N_, NP, PRE>(grid, st, SI, d, QS, Y, ldy, alpha, part);    \
     return;
   switch (nb) {
     DEIG_NB_CASE(1) DEIG_NB_CASE(2) DEIG_NB_CASE(3) DEIG_NB_CASE(4)
@@ -768,11 +811,12 @@ void launch_image(bool v3, int nb, dim3 grid, hipStream_t st, const f32x4* SI, i
 #undef DEIG_NB_CASE
 }
 
-// Workspace: [Q image][split-K slabs][S image (v2)].
+// Workspace: [Q image][split-K slabs][S image][two-piece S image] (images: v2/v3).
 struct SweepWs {
   u32x4* QS;
   float* part;
   f32x4* SI;
+  u32x4* SH;
   size_t total;
 };
 SweepWs sweep_carve(void* ws, int64_t d, int p) {
@@ -785,6 +829,8 @@ SweepWs sweep_carve(void* ws, int64_t d, int p) {
   const int ks = sweep_ks(d);
   if (ks > 1) off = align_up(off + (size_t)ks * d * p * sizeof(float), 256);
   w.SI = reinterpret_cast<f32x4*>(base + off);
+  if (sweep_version() != 1) off += si_bytes(d);
+  w.SH = reinterpret_cast<u32x4*>(base + off);
   if (sweep_version() != 1) off += si_bytes(d);
   w.total = off;
   return w;
@@ -807,7 +853,7 @@ int sweep_prepare(const float* S, int64_t d, int64_t lds, int p, void* ws, size_
   const int64_t ng = si_groups(d);
   const int64_t nunits = si_rows(d) / SI_RB * ng * 4 * 64;
   hipLaunchKernelGGL(sweep_prepare_kernel, dim3((unsigned)cdiv(nunits, 256)), dim3(256), 0, st, S,
-                     lds, d, ng, nunits, w.SI, Vd, ldv, lamd, r);
+                     lds, d, ng, nunits, w.SI, w.SH, Vd, ldv, lamd, r);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }
@@ -825,7 +871,8 @@ int sweep_round_pieces() {
 
 int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
                 float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st,
-                bool round_q) {
+                int mode) {
+  const bool round_q = mode >= 1;
   DEIG_REQUIRE(d >= 1 && p >= 16 && p <= 128 && p % 16 == 0,
                "sweep: need d >= 1 and p in {16, 32, ..., 128} (p=%d)", p);
   DEIG_REQUIRE(lds >= d && lds % 4 == 0 && lds <= (1 << 24) && ldq >= p && ldy >= p,
@@ -838,6 +885,7 @@ int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, i
   const int64_t ngrp = 2 * cdiv(d, SW_KS);
   // v1 reads the 3-piece image only.
   const int np = (round_q && sweep_version() != 1) ? sweep_round_pieces() : 3;
+  const bool pre = mode == 2 && np == 2 && sweep_version() != 1;
   const dim3 qgrid((unsigned)cdiv(ngrp * nb * 64, 256));
   if (np == 2)
     hipLaunchKernelGGL(split_q_kernel<2>, qgrid, dim3(256), 0, st, const_cast<float*>(Q), ldq, d,
@@ -861,7 +909,10 @@ int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, i
     }
   } else {
     const bool v3 = sweep_version() == 3 || (sweep_version() == 0 && nb > 5);
-    if (np == 2)
+    if (pre)
+      launch_image<2, true>(v3, nb, grid, st, reinterpret_cast<const f32x4*>(w.SH), d, w.QS, Y,
+                            ldy, alpha, w.part);
+    else if (np == 2)
       launch_image<2>(v3, nb, grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part);
     else
       launch_image<3>(v3, nb, grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part);
@@ -883,7 +934,7 @@ int sweep_launch(const float* S, int64_t d, int64_t lds, const float* Q, int p, 
                  float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st) {
   int rc = sweep_prepare(S, d, lds, p, ws, ws_bytes, st);
   if (rc) return rc;
-  return sweep_apply(S, d, lds, Q, p, ldq, Y, ldy, alpha, ws, ws_bytes, st, false);
+  return sweep_apply(S, d, lds, Q, p, ldq, Y, ldy, alpha, ws, ws_bytes, st, 0);
 }
 
 }  // namespace deig

@@ -116,6 +116,13 @@ int deig_default_subspace(int64_t d, int k);
  * bf16 pieces (16 significant bits, |Q' - Q| <= 2^-17 |Q|), and Y = alpha S Q'
  * is formed to fp32 grade from five bf16 MFMA products instead of six. */
 #define DEIG_SWEEP_ROUND_Q 0x200
+/* OR-ed into the algorithm of deig_sym_apply_f32 (BF16X6 only; implies ROUND_Q):
+ * the solver's early-sweep mode.  S is also taken as its two leading bf16 pieces
+ * (from a two-piece image written by the same prepare pass), so Y = alpha S' Q' is
+ * three bf16 MFMA products (hh + hm + mh) with no split in the sweep: ~2^-16
+ * relative (S' rounding 2^-17, dropped m m 2^-18).  deig_topk_sym_f32 uses it while
+ * its residual is above 1e-3, ROUND_Q down to 1e-4, the exact product below. */
+#define DEIG_SWEEP_FAST 0x400
 
 /* One subspace-iteration sweep Y = alpha * S Q  (S symmetric d x d row-major, lds;
  * Q d x p row-major, ldq; Y d x p row-major, ldy; p % 16 == 0, 16 <= p <= 128).

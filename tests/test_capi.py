@@ -24,6 +24,7 @@ def test_header_constants_match_bindings():
     defs = dict(re.findall(r"^#define\s+(DEIG_[A-Z0-9_]+)\s+\(?(-?(?:0x[0-9a-fA-F]+|\d+))\)?\s*$",
                            open(hdr).read(), re.M))
     assert "DEIG_SWEEP_ROUND_Q" in defs and "DEIG_SWEEP_PREPARED" in defs
+    assert "DEIG_SWEEP_FAST" in defs
     checked = 0
     for name, val in defs.items():
         if hasattr(_lib, name):

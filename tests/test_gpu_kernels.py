@@ -250,6 +250,38 @@ def test_sym_apply_round_q(d, p, cuda):
         Q = Qr
 
 
+@pytest.mark.parametrize("d,p", [(520, 80), (300, 128), (1000, 16), (8192, 80), (4100, 96)])
+def test_sym_apply_fast(d, p, cuda):
+    """The solver's early-sweep mode (DEIG_SWEEP_FAST): Q rounded in place as in
+    round_q, S taken as its two leading bf16 pieces S' = h + m from the prepared
+    two-piece image, three products hh + hm + mh.  Against float64 S' @ Q' the only
+    error is the dropped m m term (2^-18 per product) and fp32 accumulation; against
+    the exact S @ Q' it is ~2^-16 relative."""
+    import distributed_eigenspaces_amd as de
+    rng = np.random.default_rng(11 * d + p)
+    A = rng.standard_normal((d, d)).astype(np.float32)
+    S = ((A + A.T) * 0.5).astype(np.float32)
+    Q = rng.standard_normal((d, p)).astype(np.float32)
+    St = torch.from_numpy(S).to(cuda)
+    Qt = torch.from_numpy(Q).to(cuda)
+    Sh = torch.from_numpy(S).to(torch.bfloat16).float()
+    S2 = (Sh + (torch.from_numpy(S) - Sh).to(torch.bfloat16).float()).double().numpy()
+    for it in range(2):
+        Y = de.sym_apply(St, Qt, prepared=it > 0, fast=True).cpu().numpy().astype(np.float64)
+        Qr = Qt.cpu().numpy()
+        assert np.all(np.abs(Qr - Q) <= 2.0 ** -17 * np.abs(Q) * 1.0001), "rounding exceeds 2^-17"
+        ref2 = S2 @ Qr.astype(np.float64)
+        ref = S.astype(np.float64) @ Qr.astype(np.float64)
+        scale = np.abs(ref).max()
+        assert np.abs(Y - ref2).max() / scale <= 1e-5, f"fast sweep vs S'Q' d={d} p={p} it={it}"
+        assert np.abs(Y - ref).max() / scale <= 6e-5, f"fast sweep vs SQ' d={d} p={p} it={it}"
+        Q = Qr
+    # the exact modes still read the three-piece path after a fast call on one image
+    Y6 = de.sym_apply(St, Qt, prepared=True).cpu().numpy()
+    ref = S.astype(np.float64) @ Qt.cpu().numpy().astype(np.float64)
+    assert np.abs(Y6 - ref).max() / np.abs(ref).max() <= 2e-6
+
+
 def test_sym_apply_rejects_bad_p(cuda):
     import distributed_eigenspaces_amd as de
     S = torch.eye(64, device=cuda)
