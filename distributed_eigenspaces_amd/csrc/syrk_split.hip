@@ -43,6 +43,16 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Two fp32 -> packed bf16 (element 0 in the low half), round to nearest even:
+// one v_cvt_pk_bf16_f32.
+__device__ __forceinline__ uint32_t cvt2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
+}
+__device__ __forceinline__ float lo_f(uint32_t p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float hi_f(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
 
 constexpr int BT = 256;                      // tile edge (features)
 constexpr int ROWS_PAD = 32;                 // chunk rows are padded to this (2 k-steps)
@@ -72,6 +82,10 @@ struct SSched {
   int prio;      // 1: waves 4-7 run at s_setprio 1 (the arbitration losers otherwise)
   unsigned* pace;  // per-XCD arrival counters (128 B apart), zeroed per launch
   int pace_kt;     // K-tiles between two XCD pacing points (0: off)
+  // fused split (variant 163): X is staged as fp32 and split in LDS
+  const float* X;
+  int64_t ldx, nrows;
+  float* corr;  // lo^2 partials: [segment][octet wave][dp]
 };
 
 // XCD pacing point of the full-tile phases: the ~G/8 blocks on one XCD run
@@ -155,6 +169,74 @@ __device__ __forceinline__ void stage(const SSched& s, int64_t kt, int i0, int j
             buf + sl * SLICE_B + p * 1024);
     }
   }
+}
+
+// ------------------------------------------------ fused split (variant 163)
+// X is staged as it lies in HBM (fp32 rows) and split in LDS, so no XP image is
+// written and re-read (the split pass moved 2 x 4nd bytes).  A K-tile is 32 rows;
+// wave w owns octet w & 3 of panel w >> 2 (diagonal tiles: panel A twice): it
+// DMAs those 8 rows x 256 features (8 x 1 KiB) into the 8 KiB that the octet's
+// (hi, lo) slices occupy, and later overwrites them in place with the slices.
+// The region is the wave's own, so the split needs no barrier of its own.
+constexpr int OCT_B = 2 * SLICE_B;
+
+// One descriptor per stage: base = the octet's first row, records = its rows
+// below nrows (later rows read as out of range, and an out-of-range LDS-DMA
+// writes zeros); voff = 16 * lane, or an out-of-range offset (2^30 + row offset
+// >= every record count, as ldx <= 2^25) for lanes whose features are >= d.
+__device__ __forceinline__ void stage_x(const SSched& s, int64_t kt, int f0, unsigned char* buf,
+                                        int wave, int voff) {
+  const int64_t row0 = kt * 32 + 8 * (wave & 3);
+  int64_t rv = s.nrows - row0;
+  rv = rv < 0 ? 0 : rv > 8 ? 8 : rv;
+  const uint32_t ldx4 = (uint32_t)s.ldx * 4u;
+  const i32x4 rsrc = make_rsrc(s.X + row0 * s.ldx + f0, (uint32_t)rv * ldx4);
+  unsigned char* dst = buf + (wave >> 2) * Geo<2>::PANEL_B + (wave & 3) * OCT_B;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) dma16(rsrc, voff + (int)(r * ldx4), dst + r * 1024);
+}
+
+// Split the wave's staged region in place.  Lane c holds features 2c, 2c + 1 (half
+// h = 0) and 128 + 2c, 129 + 2c (h = 1) of the 8 rows; all 16 reads land before
+// the first write (the slices overlap every staged row).  Rows >= nrows and
+// features >= d are zeroed here (independent of what a dropped DMA left in LDS).
+// SQ: also accumulate the dropped lo * lo diagonal term (as r^2, r = x - hi: the
+// difference is ~2^-25 x^2) into sq[2h + e].
+template <bool SQ>
+__device__ __forceinline__ void convert_x(unsigned char* buf, int wave, int lane, int rv, int fv,
+                                          float* sq) {
+  unsigned char* R = buf + (wave >> 2) * Geo<2>::PANEL_B + (wave & 3) * OCT_B;
+  f32x2 v[2][8];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      v[h][r] = *reinterpret_cast<const f32x2*>(R + r * 1024 + h * 512 + 8 * lane);
+  if (rv < 8 || fv < 256) {  // wave-uniform: the ragged last K-tile / a panel past d
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        if (r >= rv || 128 * h + 2 * lane >= fv) v[h][r] = f32x2{0.f, 0.f};
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      u32x4 hv, lv;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const float x0 = v[h][2 * p][e], x1 = v[h][2 * p + 1][e];
+        const uint32_t hh = cvt2(x0, x1);
+        const float r0 = x0 - lo_f(hh), r1 = x1 - hi_f(hh);
+        hv[p] = hh;
+        lv[p] = cvt2(r0, r1);
+        if (SQ) sq[2 * h + e] = fmaf(r0, r0, fmaf(r1, r1, sq[2 * h + e]));
+      }
+      const int f = 128 * h + 2 * lane + e;
+      *reinterpret_cast<u32x4*>(R + f * 16) = hv;
+      *reinterpret_cast<u32x4*>(R + SLICE_B + f * 16) = lv;
+    }
 }
 
 template <int N>
@@ -306,6 +388,113 @@ struct Acc<16> {
       }
     }
   }
+
+  // Fused split (variant 163): K-tile t's MFMAs (KT = 2: one 32-deep step) with
+  // the split of this wave's region R of K-tile t + 1 woven in.  Register budget
+  // (2 waves/SIMD: 256 each, 176 held by accumulators and operands) allows 24 live
+  // fp32 inputs, so the split runs in the order the slices overwrite the staged
+  // rows: half h = 0 of the features writes hi into rows 0-1 and lo into rows 4-5,
+  // so rows {0, 1, 4, 5} (both halves) and the h = 0 halves of rows {2, 3, 6, 7}
+  // are read first (after block 1), h = 0 is split beside blocks 3-4, the h = 1
+  // halves of rows {2, 3, 6, 7} are read at block 5 and split beside blocks 6-7.
+  // The wave's LDS queue is in order, so no write overtakes an earlier read.
+  template <bool SQ>
+  __device__ __forceinline__ void split_group(unsigned char* R, int lane, int h, int e,
+                                              const f32x2 (&v)[8], float* sq) {
+    u32x4 hv, lv;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const float x0 = v[2 * p][e], x1 = v[2 * p + 1][e];
+      const uint32_t hh = cvt2(x0, x1);
+      const float r0 = x0 - lo_f(hh), r1 = x1 - hi_f(hh);
+      hv[p] = hh;
+      lv[p] = cvt2(r0, r1);
+      if (SQ) sq[2 * h + e] = fmaf(r0, r0, fmaf(r1, r1, sq[2 * h + e]));
+    }
+    const int f = 128 * h + 2 * lane + e;
+    *reinterpret_cast<u32x4*>(R + f * 16) = hv;
+    *reinterpret_cast<u32x4*>(R + SLICE_B + f * 16) = lv;
+  }
+
+  __device__ __forceinline__ void mfma_block(int mb, const bf16x8& ahi, const bf16x8& alo,
+                                             const bf16x8 (&bhi)[4], const bf16x8 (&blo)[4]) {
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+      a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi[nb], a[mb][nb], 0, 0, 0);
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+      a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, blo[nb], a[mb][nb], 0, 0, 0);
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+      a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bhi[nb], a[mb][nb], 0, 0, 0);
+  }
+
+  template <bool SQ>
+  __device__ __forceinline__ void mma_fx(const unsigned char* A, const unsigned char* B, int wi,
+                                         int wj, int lane, unsigned char* R, float* sq) {
+    const int c = lane & 15, g = lane >> 4;
+    const unsigned char* ph = A + ((g * 2) * BT + 128 * wi + c) * 16;
+    const unsigned char* qh = B + ((g * 2) * BT + 64 * wj + c) * 16;
+    bf16x8 bhi[4], blo[4], ahi[2], alo[2];
+    ahi[0] = *reinterpret_cast<const bf16x8*>(ph);
+    alo[0] = *reinterpret_cast<const bf16x8*>(ph + BT * 16);
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      bhi[nb] = *reinterpret_cast<const bf16x8*>(qh + (16 * nb) * 16);
+      blo[nb] = *reinterpret_cast<const bf16x8*>(qh + (BT + 16 * nb) * 16);
+    }
+    // region 1: blocks 0-1 (the DMAs of K-tile t + 1 are in flight)
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+      ahi[(mb + 1) & 1] = *reinterpret_cast<const bf16x8*>(ph + (16 * (mb + 1)) * 16);
+      alo[(mb + 1) & 1] = *reinterpret_cast<const bf16x8*>(ph + (BT + 16 * (mb + 1)) * 16);
+      mfma_block(mb, ahi[mb & 1], alo[mb & 1], bhi, blo);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, 10, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+    wait_vm<0>();  // this wave's DMAs of K-tile t + 1 (its own region) landed
+    // region 2: blocks 2-7 with the split
+    f32x2 v0[8], v1[8];  // h = 0 rows 0-7; h = 1 rows 0, 1, 4, 5 then 2, 3, 6, 7
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      v0[r] = *reinterpret_cast<const f32x2*>(R + r * 1024 + 8 * lane);
+      if ((r & 2) == 0) v1[r] = *reinterpret_cast<const f32x2*>(R + r * 1024 + 512 + 8 * lane);
+    }
+#pragma unroll
+    for (int mb = 2; mb < 8; ++mb) {
+      if (mb + 1 < 8) {
+        ahi[(mb + 1) & 1] = *reinterpret_cast<const bf16x8*>(ph + (16 * (mb + 1)) * 16);
+        alo[(mb + 1) & 1] = *reinterpret_cast<const bf16x8*>(ph + (BT + 16 * (mb + 1)) * 16);
+      }
+      if (mb == 5) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          if ((r & 2) != 0) v1[r] = *reinterpret_cast<const f32x2*>(R + r * 1024 + 512 + 8 * lane);
+      }
+      mfma_block(mb, ahi[mb & 1], alo[mb & 1], bhi, blo);
+      if (mb == 3 || mb == 4) split_group<SQ>(R, lane, 0, mb - 3, v0, sq);
+      if (mb == 6 || mb == 7) split_group<SQ>(R, lane, 1, mb - 6, v1, sq);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+#pragma unroll
+    for (int mb = 2; mb < 8; ++mb) {
+      if (mb + 1 < 8) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      if (mb == 5) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+      if (mb == 2 || mb == 5) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, SQ ? 3 : 2, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
+      }
+    }
+  }
 };
 
 constexpr int NQUAD = 32;
@@ -365,9 +554,10 @@ __device__ __forceinline__ void store4(const SSched& s, int ib, int j, bool diag
   }
 }
 
-template <int MF, int KT, int NST>
+template <int MF, int KT, int NST, bool FX, bool SQ>
 __device__ __forceinline__ void segment(const SSched& s, unsigned char* lds, int tile, int64_t k0, int64_t k1,
-                        int slot, bool partial, int pace_j) {
+                        int slot, bool partial, int pace_j, int cseg) {
+  static_assert(!FX || (KT == 2 && NST == 2), "fused split: 32-row K-tiles, two stages");
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wi = wave >> 2, wj = wave & 3;
@@ -376,6 +566,13 @@ __device__ __forceinline__ void segment(const SSched& s, unsigned char* lds, int
   const int ti = tt & 0xffff, tj = tt >> 16;
   const int i0 = ti * BT, j0 = tj * BT;
   const bool diag = (ti == tj);
+  // fused split: this wave's panel origin, valid features in it, DMA lane offset
+  const int fx0 = (wave >= 4 && !diag) ? j0 : i0;
+  const int fv = s.d - fx0;
+  const int xvoff = 4 * lane < fv ? lane16 : (1 << 30);
+  // lo^2 of the diagonal: panel A's octets (waves 0-3) of diagonal tiles
+  const bool sqw = SQ;
+  float sq[4] = {0.f, 0.f, 0.f, 0.f};
 
   if (s.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
   Acc<MF> acc;
@@ -391,8 +588,18 @@ __device__ __forceinline__ void segment(const SSched& s, unsigned char* lds, int
     // Ring of NST stages; NST - 1 K-tiles are issued ahead of the one being
     // computed.  Stage t lives in buffer t % NST.
     constexpr int BUF_B = Geo<KT>::BUF_B;
-    for (int t = 0; t < NST - 1 && t < nkt; ++t)
-      stage<KT>(s, k0 + t, i0, j0, diag, lds + t * BUF_B, wave, lane16);
+    if constexpr (FX) {
+      // fused: K-tile k0 staged and split (masked: it may be ragged) before the
+      // loop; iteration t stages K-tile t + 1 after the barrier and splits it
+      // inside K-tile t's MFMAs (its own region: a vmcnt wait, no barrier).
+      stage_x(s, k0, fx0, lds, wave, xvoff);
+      wait_vm<0>();
+      const int64_t rv0 = s.nrows - (k0 * 32 + 8 * (wave & 3));
+      convert_x<SQ>(lds, wave, lane, rv0 < 0 ? 0 : rv0 > 8 ? 8 : (int)rv0, fv, sq);
+    } else {
+      for (int t = 0; t < NST - 1 && t < nkt; ++t)
+        stage<KT>(s, k0 + t, i0, j0, diag, lds + t * BUF_B, wave, lane16);
+    }
     int cur = 0, nxt = NST - 1, since = 0, since_pace = 0;
     // pacing target: blocks on this XCD x arrival index
     const int xcd = blockIdx.x & 7;
@@ -408,14 +615,30 @@ __device__ __forceinline__ void segment(const SSched& s, unsigned char* lds, int
       // every reader passes.  WAR: stage t-1's ds_reads retired (lgkmcnt) before
       // the barrier, so its buffer can be restaged right after it.  A raw
       // s_barrier: __syncthreads() would drain the ring with vmcnt(0).
-      wait_stage<KT, NST>(left < NST - 2 ? (int)left : NST - 2, diag);
+      // fused: every wave split its own region of stage t last iteration (its
+      // ds_writes retire at the lgkmcnt wait), so the barrier publishes stage t.
+      if (!FX) wait_stage<KT, NST>(left < NST - 2 ? (int)left : NST - 2, diag);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (t + NST - 1 < nkt)
-        stage<KT>(s, k0 + t + NST - 1, i0, j0, diag, lds + nxt * BUF_B, wave, lane16);
-      unsigned char* bc = lds + cur * BUF_B;
-      acc.template mma<KT>(bc, diag ? bc : bc + Geo<KT>::PANEL_B, wi, wj, lane);
+      if constexpr (FX) {
+        if (t + 1 < nkt) stage_x(s, k0 + t + 1, fx0, lds + nxt * BUF_B, wave, xvoff);
+        // K-tile t's MFMAs, then this wave's split of K-tile t + 1 (its DMAs were
+        // issued right after the barrier: the MFMAs cover their latency).  The
+        // in-place split of the wave's own region needs no barrier of its own.
+        unsigned char* bc = lds + cur * BUF_B;
+        acc.template mma<KT>(bc, bc + Geo<KT>::PANEL_B, wi, wj, lane);
+        if (t + 1 < nkt) {
+          wait_vm<0>();
+          const int64_t rv1 = s.nrows - ((k0 + t + 1) * 32 + 8 * (wave & 3));
+          convert_x<SQ>(lds + nxt * BUF_B, wave, lane, rv1 < 0 ? 0 : rv1 > 8 ? 8 : (int)rv1, fv, sq);
+        }
+      } else {
+        if (t + NST - 1 < nkt)
+          stage<KT>(s, k0 + t + NST - 1, i0, j0, diag, lds + nxt * BUF_B, wave, lane16);
+        unsigned char* bc = lds + cur * BUF_B;
+        acc.template mma<KT>(bc, diag ? bc : bc + Geo<KT>::PANEL_B, wi, wj, lane);
+      }
       if (++since == s.flush_kt && t + 1 < nkt) {
         flush<MF>(slab, !flushed, acc, wave, lane);
         wait_vm<0>();  // keep the slab traffic off the ring's counted waits
@@ -427,6 +650,12 @@ __device__ __forceinline__ void segment(const SSched& s, unsigned char* lds, int
     }
   }
   if (flushed) unflush<MF>(slab, acc, wave, lane);
+  if (sqw) {  // [segment][octet wave][dp]; summed by diag_corr_kernel
+    float* c = s.corr + (int64_t)(cseg * 4 + wave) * s.dp + i0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      *reinterpret_cast<f32x2*>(c + 128 * h + 2 * lane) = f32x2{sq[2 * h], sq[2 * h + 1]};
+  }
 
   if (partial) {
 #pragma unroll
@@ -441,7 +670,7 @@ __device__ __forceinline__ void segment(const SSched& s, unsigned char* lds, int
   }
 }
 
-template <int MF, int KT, int NST>
+template <int MF, int KT, int NST, bool FX>
 __global__ __launch_bounds__(NTHR) void syrks_kernel(SSched s) {
   static_assert(NST * Geo<KT>::BUF_B <= 160 * 1024, "LDS ring exceeds 160 KiB");
   __shared__ __attribute__((aligned(16))) unsigned char lds[NST * Geo<KT>::BUF_B];
@@ -457,7 +686,7 @@ __global__ __launch_bounds__(NTHR) void syrks_kernel(SSched s) {
   const int items = s.R * s.nseg;
   const int nwork = s.q + (L < items ? (items - 1 - L) / s.G + 1 : 0);
   for (int w = 0; w < nwork; ++w) {
-    int tile, slot = 0;
+    int tile, slot = 0, cseg = 0;
     int64_t k0 = 0, k1 = s.NK;
     const bool partial = w >= s.q;
     if (!partial) {
@@ -467,6 +696,7 @@ __global__ __launch_bounds__(NTHR) void syrks_kernel(SSched s) {
       const int sg = i / s.R, r = i - sg * s.R;
       tile = s.q * s.G + r;
       slot = i;
+      cseg = sg;
       // (64-bit divisions run on the VALU: pin the bounds to SGPRs, the DMA
       // descriptors built from them must be wave-uniform)
       k0 = __builtin_amdgcn_readfirstlane((int)(s.NK * sg / s.nseg));
@@ -474,7 +704,17 @@ __global__ __launch_bounds__(NTHR) void syrks_kernel(SSched s) {
     }
     // full phases pace (identical K work on every block); remainder items do not
     const int pace_j = (!partial && s.pace_kt > 0) ? (int)(w * (s.NK / s.pace_kt)) : -1;
-    segment<MF, KT, NST>(s, lds, tile, k0, k1, slot, partial, pace_j);
+    // fused: the lo^2 accumulation is compiled only into the copy that the
+    // diagonal tiles' A-panel waves run
+    if constexpr (FX) {
+      const int tt = __builtin_amdgcn_readfirstlane(s.order[tile]);
+      if ((tt & 0xffff) == (tt >> 16) && (threadIdx.x >> 6) < 4)
+        segment<MF, KT, NST, true, true>(s, lds, tile, k0, k1, slot, partial, pace_j, cseg);
+      else
+        segment<MF, KT, NST, true, false>(s, lds, tile, k0, k1, slot, partial, pace_j, cseg);
+    } else {
+      segment<MF, KT, NST, false, false>(s, lds, tile, k0, k1, slot, partial, pace_j, cseg);
+    }
   }
 }
 
@@ -633,10 +873,25 @@ int64_t default_chunk_rows(int64_t n, int64_t d) {
   return n32 < cap ? n32 : cap;
 }
 
+// Kernel shape: 163 = fused split (X staged as fp32 and split in LDS), 162 = split
+// pass + MFMA 16x16x32, 22 / 13 | 14 | 15 = split pass + 32x32x16 (2 k-steps per
+// K-tile x 2 stages; 1 k-step x 3 | 4 | 5 stages).  Default by width: the fused
+// split re-splits each panel once per tile that reads it (~d / 256 times), the
+// split pass once (2 x 4nd bytes), so the split pass's share of the op falls as
+// 1/d while the fused split's stays.  Measured (r02, interleaved A/B in one
+// process, profiles/r02l_syrk_fused_ab.log): d = 3072 (config 2) fused 27.3 ms vs
+// 29.0 ms; d = 8192 (config 3 shard) fused 370 ms vs 336 ms.
+// DEIG_SYRK_VARIANT selects one for A/B measurements.
+int syrk_variant(int64_t d) {
+  if (const char* v = getenv("DEIG_SYRK_VARIANT")) return atoi(v);
+  return d <= 4096 ? 163 : 162;
+}
+
 }  // namespace
 
 size_t syrk_split_workspace_bytes(int64_t n, int64_t d) {
   if (n < 1 || d < 1) return 0;
+  if (syrk_variant(d) == 163) return make_layout(n, d, num_cus(), 0).total;
   return make_layout(n, d, num_cus(), default_chunk_rows(n, d)).total;
 }
 
@@ -650,15 +905,17 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
   DEIG_REQUIRE(lds >= d && lds % 4 == 0, "syrk: lds must be >= d and a multiple of 4");
   DEIG_REQUIRE(X && S && aligned16(X) && aligned16(S), "syrk: X and S must be 16-byte aligned");
   const int G = num_cus();
+  const int variant = syrk_variant(d);
+  const bool fused = variant == 163;
   // Largest chunk (multiple of 32 rows, <= n rounded up) that fits the workspace.
   Layout L0 = make_layout(n, d, G, 0);
-  if (!ws || ws_bytes < L0.total + (size_t)ROWS_PAD * L0.dp * 4)
-    return fail(DEIG_EWORKSPACE, "syrk: workspace %zu bytes < minimum %zu", ws_bytes,
-                L0.total + (size_t)ROWS_PAD * L0.dp * 4);
+  const size_t ws_min = L0.total + (fused ? 0 : (size_t)ROWS_PAD * L0.dp * 4);
+  if (!ws || ws_bytes < ws_min)
+    return fail(DEIG_EWORKSPACE, "syrk: workspace %zu bytes < minimum %zu", ws_bytes, ws_min);
   int64_t chunk = (int64_t)((ws_bytes - L0.total) / (size_t)(L0.dp * 4)) / ROWS_PAD * ROWS_PAD;
   const int64_t n32 = cdiv(n, ROWS_PAD) * ROWS_PAD;
   if (chunk > n32) chunk = n32;
-  const Layout L = make_layout(n, d, G, chunk);
+  const Layout L = make_layout(n, d, G, fused ? 0 : chunk);
   char* base = static_cast<char*>(ws);
 
   SSched s;
@@ -679,11 +936,6 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
   float* corr = reinterpret_cast<float*>(base + L.off_corr);
   unsigned char* xp = reinterpret_cast<unsigned char*>(base + L.off_xp);
 
-  // Kernel shape: MFMA 16x16x32 (variant 162) or 32x32x16 (22: 2 k-steps per
-  // K-tile x 2 stages; 13 | 14 | 15: 1 k-step x 3 | 4 | 5 stages).
-  // DEIG_SYRK_VARIANT selects one for A/B measurements.
-  int variant = 162;
-  if (const char* v = getenv("DEIG_SYRK_VARIANT")) variant = atoi(v);
   // Two-level fp32 summation: accumulators are added into a per-block slab
   // every flush_rows rows (DEIG_SYRK_FLUSH_ROWS overrides, for A/B runs).
   int64_t flush_rows = 4096;
@@ -702,6 +954,33 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
   hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(64), 0, stream, s.nt,
                      reinterpret_cast<int*>(base + L.off_order));
   DEIG_HIP_CHECK(hipGetLastError());
+  s.X = X;
+  s.ldx = ldx;
+  s.nrows = n;
+  s.corr = corr;
+  if (fused) {
+    DEIG_REQUIRE(ldx <= (int64_t(1) << 25), "syrk: ldx > 2^25 needs DEIG_SYRK_VARIANT=162");
+    // One pass over all n rows (no XP image, no chunks).  lo^2 partials:
+    // [segment < max(1, nseg)][octet wave < 4][dp], zero where no diagonal tile wrote.
+    const int64_t yb = 4 * (L.nseg > 1 ? L.nseg : 1);
+    DEIG_HIP_CHECK(hipMemsetAsync(corr, 0, sizeof(float) * (size_t)(yb * L.dp), stream));
+    s.NK = cdiv(n, ROWS_PAD);
+    s.nseg = (int)L.nseg;
+    s.beta = 0;
+    s.flush_kt = (int)(flush_rows / ROWS_PAD);
+    if (s.flush_kt < 1) s.flush_kt = 1;
+    if (s.pace_kt > 0) DEIG_HIP_CHECK(hipMemsetAsync(s.pace, 0, 8 * 128, stream));
+    hipLaunchKernelGGL((syrks_kernel<16, 2, 2, true>), dim3(G), dim3(NTHR), 0, stream, s);
+    DEIG_HIP_CHECK(hipGetLastError());
+    if (s.R > 0) {
+      hipLaunchKernelGGL(syrks_reduce_kernel<16>, dim3(s.R, SLAB / 4 / 256), dim3(256), 0, stream, s);
+      DEIG_HIP_CHECK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(diag_corr_kernel, dim3((unsigned)cdiv(d, 256)), dim3(256), 0, stream, corr,
+                       (int)yb, L.dp, (int)d, alpha, S, lds);
+    DEIG_HIP_CHECK(hipGetLastError());
+    return DEIG_OK;
+  }
   for (int64_t r0 = 0, c = 0; r0 < n; r0 += chunk, ++c) {
     const int64_t rows = (n - r0) < chunk ? (n - r0) : chunk;
     const int64_t nk32 = cdiv(rows, ROWS_PAD);  // 32-row blocks (zero-padded)
@@ -720,11 +999,11 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
     const bool mf16 = variant >= 100;
     if (s.pace_kt > 0) DEIG_HIP_CHECK(hipMemsetAsync(s.pace, 0, 8 * 128, stream));
     switch (variant) {
-      case 13: hipLaunchKernelGGL((syrks_kernel<32, 1, 3>), dim3(G), dim3(NTHR), 0, stream, s); break;
-      case 14: hipLaunchKernelGGL((syrks_kernel<32, 1, 4>), dim3(G), dim3(NTHR), 0, stream, s); break;
-      case 15: hipLaunchKernelGGL((syrks_kernel<32, 1, 5>), dim3(G), dim3(NTHR), 0, stream, s); break;
-      case 22: hipLaunchKernelGGL((syrks_kernel<32, 2, 2>), dim3(G), dim3(NTHR), 0, stream, s); break;
-      default: hipLaunchKernelGGL((syrks_kernel<16, 2, 2>), dim3(G), dim3(NTHR), 0, stream, s); break;
+      case 13: hipLaunchKernelGGL((syrks_kernel<32, 1, 3, false>), dim3(G), dim3(NTHR), 0, stream, s); break;
+      case 14: hipLaunchKernelGGL((syrks_kernel<32, 1, 4, false>), dim3(G), dim3(NTHR), 0, stream, s); break;
+      case 15: hipLaunchKernelGGL((syrks_kernel<32, 1, 5, false>), dim3(G), dim3(NTHR), 0, stream, s); break;
+      case 22: hipLaunchKernelGGL((syrks_kernel<32, 2, 2, false>), dim3(G), dim3(NTHR), 0, stream, s); break;
+      default: hipLaunchKernelGGL((syrks_kernel<16, 2, 2, false>), dim3(G), dim3(NTHR), 0, stream, s); break;
     }
     DEIG_HIP_CHECK(hipGetLastError());
     if (s.R > 0) {

@@ -87,3 +87,16 @@ def test_no_cpu_fallback():
         de.sigma_hat(torch.ones(4, 4))
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         de.topk_eigh(torch.eye(16), 2)
+
+
+def test_workspace_fused_split_variant(monkeypatch):
+    """d <= 4096 (config 2) defaults to the fused split, which stages X itself: no
+    image of the shard in the workspace; DEIG_SYRK_VARIANT=162 brings it back."""
+    L = _lib.lib()
+    n, d = 1 << 20, 3072
+    ws = L.deig_syrk_workspace_ex(n, d, _lib.DEIG_SYRK_SPLIT3)
+    assert 0 < ws < n * d * 4 // 10  # slabs only (the image would be n * d * 4)
+    monkeypatch.setenv("DEIG_SYRK_VARIANT", "162")
+    assert L.deig_syrk_workspace_ex(n, d, _lib.DEIG_SYRK_SPLIT3) >= n * d * 4
+    monkeypatch.setenv("DEIG_SYRK_VARIANT", "163")
+    assert L.deig_syrk_workspace_ex(1 << 21, 8192, _lib.DEIG_SYRK_SPLIT3) < (1 << 30)

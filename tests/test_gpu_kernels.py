@@ -52,9 +52,11 @@ def test_syrk_shapes(n, d, algo, cuda):
     _syrk_check(X, cuda, rel=tol, algo=algo)
 
 
-def test_syrk_split3_chunked_accumulation(cuda):
-    """A workspace that holds one 32-row chunk: the split3 path then runs
-    ceil(n/32) split + SYRK + diagonal-correction rounds accumulating into S."""
+def test_syrk_split3_chunked_accumulation(cuda, monkeypatch):
+    """Split-pass variant (162) with a workspace that holds one 32-row chunk: it
+    then runs ceil(n/32) split + SYRK + diagonal-correction rounds accumulating
+    into S.  (The default fused variant needs no XP image and never chunks.)"""
+    monkeypatch.setenv("DEIG_SYRK_VARIANT", "162")
     import ctypes
     from distributed_eigenspaces_amd import _lib
     L = _lib.lib()
@@ -78,6 +80,43 @@ def test_syrk_split3_chunked_accumulation(cuda):
                             _lib.DEIG_SYRK_SPLIT3, ws.data_ptr(), 1024,
                             torch.cuda.current_stream().cuda_stream)
     assert rc == _lib.DEIG_EWORKSPACE
+
+
+@pytest.mark.parametrize("n,d", [(1, 4), (33, 64), (1000, 520), (4097, 1000), (5000, 3072)])
+def test_syrk_fused_split_matches_split_pass(n, d, cuda, monkeypatch):
+    """The fused split (X staged as fp32 and split in LDS, variant 163, default)
+    forms the same bf16 pieces and MFMA sums as the split pass (162): equal up to
+    the order of the diagonal lo^2 correction sums."""
+    import distributed_eigenspaces_amd as de
+    rng = np.random.default_rng(n + 3 * d)
+    X = (rng.standard_normal((n, d)) * 2 + 0.5).astype(np.float32)
+    x = torch.from_numpy(X).to(cuda)
+    out = {}
+    for v in ("163", "162"):
+        monkeypatch.setenv("DEIG_SYRK_VARIANT", v)
+        out[v] = de.sigma_hat(x, algo="split3").cpu().numpy().astype(np.float64)
+    Sr = ref_cpu.sigma_hat(X.astype(np.float64))
+    scale = np.abs(Sr).max()
+    assert np.abs(out["163"] - Sr).max() <= _split3_tol(n) * scale
+    off = ~np.eye(d, dtype=bool)
+    assert np.array_equal(out["163"][off], out["162"][off]), "off-diagonal sums must be identical"
+    assert np.abs(np.diag(out["163"]) - np.diag(out["162"])).max() <= 1e-6 * scale
+    assert np.array_equal(out["163"], out["163"].T)
+
+
+def test_syrk_fused_split_strided_nan_padding(cuda):
+    """Rows strided (ldx > d) with NaN in the padding columns and d not a multiple
+    of the 256-feature panel: the fused split reads only features < d."""
+    import distributed_eigenspaces_amd as de
+    rng = np.random.default_rng(5)
+    n, d, ldx = 3000, 300, 312
+    big = np.full((n, ldx), np.nan, dtype=np.float32)
+    big[:, :d] = rng.standard_normal((n, d)).astype(np.float32)
+    view = torch.from_numpy(big).to(cuda)[:, :d]
+    S = de.sigma_hat(view, algo="split3").cpu().numpy().astype(np.float64)
+    Sr = ref_cpu.sigma_hat(big[:, :d].astype(np.float64))
+    assert np.isfinite(S).all()
+    assert np.abs(S - Sr).max() <= 2e-6 * np.abs(Sr).max()
 
 
 def test_syrk_split3_integer_data_exact_split(cuda):
