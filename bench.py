@@ -262,8 +262,21 @@ def sweep_roofline(de, S: torch.Tensor, p: int, stream) -> dict:
                      "fp32_equiv_tflops": fl / t / 1e12, "attainable_frac": t_min / t}
         if nprod:
             out[algo]["image_prepare_us_once_per_solve"] = max(prep_ms - ms, 0.0) * 1e3
-    out["kernel"] = ("split_q_kernel + sweep2_kernel (p <= 80) / sweep3_kernel (p > 80) (+ "
-                     "sweep_reduce_kernel) on the S images (sweep_prepare_kernel, once per solve): "
+            # the solver's cost per sweep: inside its chain each basis step is fused
+            # with the split-K reduction and the next sweep's Q image (sym_power:
+            # sweep kernel + sweep_finish_kernel per sweep, launched from C)
+            # (scaled by 1 / the Gershgorin bound: the chain neither overflows nor dies out)
+            cs = torch.full((p,), 1.0, device=S.device) / S.abs().sum(1).max()
+            Qc = Q.clone()
+            nst = 10
+            cms = time_events(lambda: de.sym_power(S, Qc, cs, nst, out=Y, prepared=True,
+                                                   round_q=rq, fast=fa), 3, stream) / nst
+            out[algo]["in_solver_chain_us"] = cms * 1e3
+            out[algo]["in_solver_chain_hbm_frac"] = byt / (cms * 1e-3) / HBM_PEAK
+    out["kernel"] = ("us: split_q_kernel + sweep2_kernel (p <= 80) / sweep3_kernel (p > 80) (+ "
+                     "sweep_reduce_kernel), one standalone product; in_solver_chain_us: sweep kernel "
+                     "+ sweep_finish_kernel (split-K reduction, power step and next Q image fused), "
+                     "per sweep of a 10-sweep chain; on the S images (sweep_prepare_kernel, once per solve): "
                      "bf16x3 = 3 bf16 MFMA 16x16x32 products of the prepared two-piece S image and "
                      "two-piece Q; bf16x5 / bf16x6 = 5 / 6 products of S rows split into 3 pieces "
                      "in registers and 2- / 3-piece Q; fp32: skinny_kernel<T> f32 MFMA 16x16x4")

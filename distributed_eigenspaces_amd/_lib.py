@@ -72,6 +72,9 @@ SIGNATURES = {
                                           _vp]),
     "deig_sym_apply_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _fp, ctypes.c_int, _c_i64, _fp,
                                           _c_i64, ctypes.c_float, ctypes.c_int, _vp, _c_sz, _vp]),
+    "deig_sym_power_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _fp, ctypes.c_int, _c_i64, _fp,
+                                          _c_i64, _fp, ctypes.c_int, ctypes.c_int, _vp, _c_sz,
+                                          _vp]),
     "deig_sym_apply_workspace": (_c_sz, [_c_i64, ctypes.c_int, ctypes.c_int]),
     "deig_project_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, _fp, ctypes.c_int, _c_i64,
                                         _fp, _c_i64, _vp, _c_sz, _vp]),

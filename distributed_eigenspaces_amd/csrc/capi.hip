@@ -133,24 +133,44 @@ SolverWs carve_solver(void* ws, size_t cap, int64_t d, int k, int p, int64_t mk,
   return w;
 }
 
-int apply_op(const Operator& op, const SolverWs& w, int64_t d, int p, hipStream_t st,
-             int smode) {
+// Y = A Q without a sweep image: the fp32 skinny product (explicit S) or the
+// implicit projector average Wt^T (Wt Q) (the server).
+int apply_op_plain(const Operator& op, const SolverWs& w, int64_t d, int p, hipStream_t st) {
   float* Q = w.rr.Z;
   float* Y = w.rr.Z + p;
   const int64_t ld = 2 * p;
-  if (!op.implicit) {
-    if (w.sweep_ws)
-      return sweep_apply(op.S, d, op.lds, Q, p, ld, Y, ld, 1.f, w.sweep_ws, w.sweep_bytes, st,
-                         smode);
+  if (!op.implicit)
     return skinny_launch(true, op.S, op.lds, Q, ld, Y, ld, d, p, d, 1.f, 0.f, w.slab,
                          w.slab_bytes, st);
-  }
   int rc = skinny_launch(false, op.Wt, op.ldw, Q, ld, w.Zt, p, op.mk, p, d, 1.f, 0.f, w.slab,
                          w.slab_bytes, st);
   if (rc) return rc;
   return skinny_launch(true, op.Wt, op.ldw, w.Zt, p, Y, ld, d, p, op.mk, op.scale, 0.f, w.slab,
                        w.slab_bytes, st);
 }
+
+// Y = A Q.  step (optional): the basis step that follows (power / Chebyshev).  On
+// the sweep path it is fused into the sweep's split-K reduction together with the
+// next sweep's Q image, and q_ready says that this sweep's image was written by
+// the previous one (sweep.hip sweep_finish_kernel); elsewhere it runs as its own
+// kernel after the product.
+int apply_op(const Operator& op, const SolverWs& w, int64_t d, int p, hipStream_t st, int smode,
+             const SweepStep* step = nullptr, bool q_ready = false) {
+  float* Q = w.rr.Z;
+  float* Y = w.rr.Z + p;
+  const int64_t ld = 2 * p;
+  if (!op.implicit && w.sweep_ws)
+    return sweep_apply(op.S, d, op.lds, Q, p, ld, Y, ld, 1.f, w.sweep_ws, w.sweep_bytes, st,
+                       smode, step, q_ready);
+  int rc = apply_op_plain(op, w, d, p, st);
+  if (rc || !step) return rc;
+  if (step->kind == 1) return rr_power_launch(w.rr, d, p, step->tau, st);
+  return cheb_step_launch(w.rr, w.T, d, p, step->thr, step->a, step->cc, step->gamma, st);
+}
+
+// Whether apply_op fuses steps and Q images (the q_ready protocol applies).
+bool fused_steps(const Operator& op, const SolverWs& w) { return !op.implicit && w.sweep_ws; }
+
 
 // Chebyshev filter plan for the sweeps between two Rayleigh-Ritz steps (host side,
 // from the last RR's Ritz values theta_0 >= ... >= theta_{p-1} and residual).
@@ -273,13 +293,22 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
                                                                          : kSweepExact;
       ChebPlan plan;
       const bool cheb = cheb_on && nrr > 0 && cheb_plan(lam_h, kc, p, last, tol, &plan);
-      int ncheb = 0, rc2;
+      int ncheb = 0, nstep = 0, rc2;
+      // every sweep of a cycle runs in smode, so a fused step can write the next
+      // sweep's Q image (q_ready from the second sweep of the cycle on)
+      const bool fuse = fused_steps(op, w);
+      SweepStep step{};
+      step.Q = w.rr.Z;
+      step.ldq = 2 * p;
+      step.T = w.T;
+      step.cs = w.rr.cs;
+      step.lam = w.rr.lam;
+      step.next_mode = smode;
       if (cheb) {
         // degree j: apply A to X_j, then X_{j+1} from X_j, A X_j and X_{j-1}
         const int m = std::min(plan.m, max_sweeps - it - 1);
         double s_prev = plan.s1;
-        for (int j = 0; j < m; ++j, ++it) {
-          if ((rc2 = apply_op(op, w, d, p, st, smode))) return rc2;
+        for (int j = 0; j < m; ++j, ++it, ++nstep) {
           double alpha, gamma;
           if (j == 0) {
             alpha = plan.s1 / plan.e;
@@ -290,20 +319,23 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
             gamma = s_prev * s_next;
             s_prev = s_next;
           }
-          if ((rc2 = cheb_step_launch(w.rr, w.T, d, p, plan.thr, (float)alpha, (float)plan.cc,
-                                      (float)gamma, st)))
-            return rc2;
+          step.kind = 2;
+          step.thr = plan.thr;
+          step.a = (float)alpha;
+          step.cc = (float)plan.cc;
+          step.gamma = (float)gamma;
+          if ((rc2 = apply_op(op, w, d, p, st, smode, &step, fuse && nstep > 0))) return rc2;
         }
         ncheb = m;
       } else if (nrr > 0) {
         const int npow = std::min(rr_every - 1, max_sweeps - it - 1);
-        for (int j = 0; j < npow; ++j, ++it) {
-          if ((rc2 = apply_op(op, w, d, p, st, smode))) return rc2;
-          // power step on the live Ritz columns of the last RR (Q_j <- Y_j / ||Y w_j||)
-          if ((rc2 = rr_power_launch(w.rr, d, p, tau, st))) return rc2;
-        }
+        // power steps on the live Ritz columns of the last RR (Q_j <- Y_j / ||Y w_j||)
+        step.kind = 1;
+        step.tau = tau;
+        for (int j = 0; j < npow; ++j, ++it, ++nstep)
+          if ((rc2 = apply_op(op, w, d, p, st, smode, &step, fuse && nstep > 0))) return rc2;
       }
-      if ((rc2 = apply_op(op, w, d, p, st, smode))) return rc2;
+      if ((rc2 = apply_op(op, w, d, p, st, smode, nullptr, fuse && nstep > 0))) return rc2;
       ++it;
       if ((rc2 = skinny_launch(true, w.rr.Z, 2 * p, w.rr.Z, 2 * p, w.rr.C, 2 * p, 2 * p, 2 * p,
                                d, 1.f, 0.f, w.slab, w.slab_bytes, st)))
@@ -508,6 +540,39 @@ int deig_projavg_topk_f32(const float* Wt, int64_t d, int64_t mk, int64_t ldw, f
   op.scale = scale;
   return solve(op, d, k, p, max_sweeps, tol, Q0, k0, ldq0, V, ldv, evals, sweeps_out, resid_out,
                ws, ws_bytes, (hipStream_t)stream);
+}
+
+int deig_sym_power_f32(const float* S, int64_t d, int64_t lds, float* Q, int p, int64_t ldq,
+                       float* Y, int64_t ldy, const float* cs, int steps, int algo, void* ws,
+                       size_t ws_bytes, void* stream) {
+  g_err[0] = 0;
+  DEIG_REQUIRE(steps >= 1 && cs && Q, "sym_power: need steps >= 1, cs and Q");
+  const bool prepared = (algo & DEIG_SWEEP_PREPARED) != 0;
+  const int smode = (algo & DEIG_SWEEP_FAST)      ? kSweepFast
+                    : (algo & DEIG_SWEEP_ROUND_Q) ? kSweepRoundQ
+                                                  : kSweepExact;
+  algo &= ~(DEIG_SWEEP_PREPARED | DEIG_SWEEP_ROUND_Q | DEIG_SWEEP_FAST);
+  if (algo != DEIG_SWEEP_AUTO && algo != DEIG_SWEEP_BF16X6)
+    return fail(DEIG_EINVAL, "sym_power: algorithm %d has no fused chain (bf16x6 only)", algo);
+  hipStream_t st = (hipStream_t)stream;
+  if (!prepared) {
+    const int rc = sweep_prepare(S, d, lds, p, ws, ws_bytes, st);
+    if (rc) return rc;
+  }
+  SweepStep step{};
+  step.kind = 1;
+  step.Q = Q;
+  step.ldq = ldq;
+  step.cs = cs;
+  step.lam = cs;  // liveness |cs_j| >= 0 * |cs_0|: every column with cs_j > 0
+  step.tau = 0.f;
+  step.next_mode = smode;
+  for (int i = 0; i < steps; ++i) {
+    const int rc = sweep_apply(S, d, lds, Q, p, ldq, Y, ldy, 1.f, ws, ws_bytes, st, smode, &step,
+                               i > 0);
+    if (rc) return rc;
+  }
+  return DEIG_OK;
 }
 
 size_t deig_sym_apply_workspace(int64_t d, int p, int algo) {

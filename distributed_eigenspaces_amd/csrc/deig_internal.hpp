@@ -109,9 +109,25 @@ int sweep_version();
 // two leading bf16 pieces from the prepared two-piece image - three products, no
 // split in the sweep, ~2^-16 relative.
 constexpr int kSweepExact = 0, kSweepRoundQ = 1, kSweepFast = 2;
+// Optional epilogue of a sweep in the solver's chain, fused with the split-K
+// reduction (sweep_finish_kernel): the basis step that turns Y = S Q into the next
+// Q (the elementwise rr_power_kernel / cheb_step_kernel forms), and the next
+// sweep's Q image (next_mode: the mode of the sweep that will read it, which then
+// runs with q_ready and skips its own split_q_kernel).
+struct SweepStep {
+  int kind;  // 1 = power (Q_j <- Y_j cs_j on live columns), 2 = Chebyshev degree
+  float* Q;  // the basis (row stride ldq), updated in place
+  int64_t ldq;
+  float* T;  // Chebyshev: X_{j-1} (row stride p)
+  const float* cs;
+  const float* lam;
+  float tau;                // power: live if cs_j > 0 and |lam_j| >= tau |lam_0|
+  float thr, a, cc, gamma;  // Chebyshev: X_{j+1} = a (Y - cc X_j) - gamma X_{j-1} if lam_j >= thr
+  int next_mode;            // kSweep* of the next sweep
+};
 int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
                 float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st,
-                int mode = kSweepExact);
+                int mode = kSweepExact, const SweepStep* step = nullptr, bool q_ready = false);
 
 // Rayleigh-Ritz pieces (rr.hip).
 struct RRBuffers {

@@ -702,6 +702,97 @@ __global__ __launch_bounds__(256) void sweep_reduce_kernel(const float* __restri
   *reinterpret_cast<fv*>(Y + m * ldy + n) = alpha * s;
 }
 
+// Split-K reduction of one sweep fused with the solver's basis step and the next
+// sweep's Q image: replaces sweep_reduce_kernel + rr_power_kernel / cheb_step_kernel
+// + split_q_kernel (three launches and their kernel boundaries per sweep).  One
+// block per 8-row octet of the image (4 per k-group), 2p threads (rounded up to
+// whole waves).  Phase 1 (row-major, one float4 of columns per thread, all ks slab
+// loads issued together): Y = alpha sum_s part_s in slab order (ks == 1: Y as the
+// sweep wrote it), the step, the new basis rounded to h + m when the next sweep
+// takes two pieces (as split_q_kernel<2> rounds it), staged in LDS; phase 2
+// (split_q_kernel's mapping, p threads): the octet's image units.
+template <int NP>
+__global__ __launch_bounds__(256) void sweep_finish_kernel(const float* __restrict__ part, int ks,
+                                                           int64_t d, int p, float alpha,
+                                                           float* __restrict__ Y, int64_t ldy,
+                                                           SweepStep st, int nb,
+                                                           u32x4* __restrict__ QS) {
+  __shared__ float qt[8][132];
+  const int64_t g = blockIdx.x >> 2;
+  const int o = blockIdx.x & 3;
+  const int pq = p >> 2;
+  const int u = threadIdx.x;
+  if (u < 8 * pq) {
+    const int rr = u / pq, c4 = (u - rr * pq) * 4;
+    const int64_t r = 32 * g + 8 * o + rr;
+    f32x4 qn = {0.f, 0.f, 0.f, 0.f};
+    if (r < d) {
+      f32x4 y;
+      if (ks > 1) {
+        const float* pp = part + r * p + c4;
+        const int64_t sd = d * p;
+        f32x4 v[8];
+        y = *reinterpret_cast<const f32x4*>(pp);
+        for (int k0 = 1; k0 < ks; k0 += 8) {  // loads of a group issued together
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (k0 + k < ks) v[k] = *reinterpret_cast<const f32x4*>(pp + (k0 + k) * sd);
+#pragma unroll
+          for (int k = 0; k < 8; ++k)  // fixed order: deterministic
+            if (k0 + k < ks) y += v[k];
+        }
+        y *= alpha;
+        *reinterpret_cast<f32x4*>(Y + r * ldy + c4) = y;
+      } else {
+        y = *reinterpret_cast<const f32x4*>(Y + r * ldy + c4);
+      }
+      f32x4* qp = reinterpret_cast<f32x4*>(st.Q + r * st.ldq + c4);
+      const f32x4 q = *qp;
+      qn = q;
+      if (st.kind == 1) {
+        const float l0 = fabsf(st.lam[0]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float c = st.cs[c4 + e];
+          if (c > 0.f && fabsf(st.lam[c4 + e]) >= st.tau * l0) qn[e] = y[e] * c;
+        }
+      } else {
+        f32x4* tp = reinterpret_cast<f32x4*>(st.T + r * p + c4);
+        // degree 1 (gamma == 0) must not read T: uninitialised workspace then
+        const f32x4 t = st.gamma != 0.f ? *tp : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (st.lam[c4 + e] >= st.thr) qn[e] = st.a * (y[e] - st.cc * q[e]) - st.gamma * t[e];
+        *tp = q;
+      }
+      if (NP == 2) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const uint32_t h = cvt2(qn[2 * e], qn[2 * e + 1]);
+          const uint32_t m = cvt2(qn[2 * e] - lo_f(h), qn[2 * e + 1] - hi_f(h));
+          qn[2 * e] = lo_f(h) + lo_f(m);
+          qn[2 * e + 1] = hi_f(h) + hi_f(m);
+        }
+      }
+      *qp = qn;
+    }
+    *reinterpret_cast<f32x4*>(&qt[rr][c4]) = qn;
+  }
+  __syncthreads();
+  if (u < p) {
+    const int j = u >> 4, n = u;
+    const f32x4 a = {qt[0][n], qt[1][n], qt[2][n], qt[3][n]};
+    const f32x4 b = {qt[4][n], qt[5][n], qt[6][n], qt[7][n]};
+    u32x4 hi, mi, lo;
+    split8(a, b, hi, mi, lo);
+    const int64_t tt = g * nb + j;
+    const int lane = 16 * o + (u & 15);
+    QS[(tt * NP + 0) * 64 + lane] = hi;
+    QS[(tt * NP + 1) * 64 + lane] = mi;
+    if constexpr (NP == 3) QS[(tt * NP + 2) * 64 + lane] = lo;
+  }
+}
+
 int sweep_bpc() {
   static int v = -1;
   if (v < 0) {
@@ -871,7 +962,7 @@ int sweep_round_pieces() {
 
 int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
                 float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st,
-                int mode) {
+                int mode, const SweepStep* step, bool q_ready) {
   const bool round_q = mode >= 1;
   DEIG_REQUIRE(d >= 1 && p >= 16 && p <= 128 && p % 16 == 0,
                "sweep: need d >= 1 and p in {16, 32, ..., 128} (p=%d)", p);
@@ -887,13 +978,16 @@ int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, i
   const int np = (round_q && sweep_version() != 1) ? sweep_round_pieces() : 3;
   const bool pre = mode == 2 && np == 2 && sweep_version() != 1;
   const dim3 qgrid((unsigned)cdiv(ngrp * nb * 64, 256));
-  if (np == 2)
-    hipLaunchKernelGGL(split_q_kernel<2>, qgrid, dim3(256), 0, st, const_cast<float*>(Q), ldq, d,
-                       nb, ngrp, w.QS);
-  else
-    hipLaunchKernelGGL(split_q_kernel<3>, qgrid, dim3(256), 0, st, const_cast<float*>(Q), ldq, d,
-                       nb, ngrp, w.QS);
-  DEIG_HIP_CHECK(hipGetLastError());
+  // q_ready: the previous sweep's finish kernel already wrote this Q's image
+  if (!q_ready) {
+    if (np == 2)
+      hipLaunchKernelGGL(split_q_kernel<2>, qgrid, dim3(256), 0, st, const_cast<float*>(Q), ldq, d,
+                         nb, ngrp, w.QS);
+    else
+      hipLaunchKernelGGL(split_q_kernel<3>, qgrid, dim3(256), 0, st, const_cast<float*>(Q), ldq, d,
+                         nb, ngrp, w.QS);
+    DEIG_HIP_CHECK(hipGetLastError());
+  }
   const int ks = sweep_ks(d);
   const dim3 grid((unsigned)(cdiv(d, SW_ROWS) * ks));
   if (sweep_version() == 1) {
@@ -918,6 +1012,22 @@ int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, i
       launch_image<3>(v3, nb, grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part);
   }
   DEIG_HIP_CHECK(hipGetLastError());
+  if (step) {
+    DEIG_REQUIRE(ldy % 4 == 0 && aligned16(Y) && step->ldq % 4 == 0 && aligned16(step->Q) &&
+                     (step->kind == 1 || step->kind == 2),
+                 "sweep: fused step needs 16-byte aligned Y / Q rows");
+    const int nnp = (step->next_mode >= kSweepRoundQ && sweep_version() != 1) ? sweep_round_pieces() : 3;
+    const float* pp = ks > 1 ? w.part : nullptr;
+    const dim3 fgrid((unsigned)(4 * ngrp)), fblk((unsigned)((2 * p + 63) / 64 * 64));
+    if (nnp == 2)
+      hipLaunchKernelGGL(sweep_finish_kernel<2>, fgrid, fblk, 0, st, pp, ks, d, p, alpha, Y, ldy,
+                         *step, nb, w.QS);
+    else
+      hipLaunchKernelGGL(sweep_finish_kernel<3>, fgrid, fblk, 0, st, pp, ks, d, p, alpha, Y, ldy,
+                         *step, nb, w.QS);
+    DEIG_HIP_CHECK(hipGetLastError());
+    return DEIG_OK;
+  }
   if (ks > 1) {
     if (ldy % 4 == 0 && aligned16(Y))
       hipLaunchKernelGGL(sweep_reduce_kernel<4>, dim3((unsigned)cdiv(d * p / 4, 256)), dim3(256),

@@ -23,7 +23,7 @@ from . import _lib
 __all__ = [
     "sigma_hat", "topk_eigh", "projavg_topk", "oja_step", "default_subspace",
     "EigResult", "require_device_tensor", "project", "stack_bases", "gemm_skinny",
-    "oja_steps", "sym_apply", "sigma_hat_u8",
+    "oja_steps", "sym_apply", "sym_power", "sigma_hat_u8",
 ]
 
 DEFAULT_TOL = 1e-6
@@ -480,6 +480,48 @@ def sym_apply(S: torch.Tensor, Q: torch.Tensor, algo: str = "auto", alpha: float
                                   Y.data_ptr(), Y.stride(0), ctypes.c_float(alpha), code,
                                   ws.data_ptr(), nbytes, _stream(S.device))
     _lib.check(rc, "deig_sym_apply_f32")
+    return Y
+
+
+def sym_power(S: torch.Tensor, Q: torch.Tensor, cs: torch.Tensor, steps: int,
+              out: torch.Tensor | None = None, prepared: bool = False,
+              round_q: bool = False, fast: bool = False) -> torch.Tensor:
+    """``steps`` sweeps of the solver's power chain (include/deig.h
+    deig_sym_power_f32): Y = S Q, then Q_j <- cs_j Y_j on the columns with
+    cs_j > 0, each step fused into the sweep's split-K reduction with the next
+    sweep's Q image, as between the Rayleigh-Ritz steps of ``topk_eigh``.  Q
+    (contiguous float32, d x p) is updated in place; returns Y = S Q_{steps-1}.
+    Flags as for ``sym_apply`` (bf16x6 only)."""
+    round_q = round_q or fast
+    S = require_device_tensor(S, "sym_power")
+    Q = require_device_tensor(Q, "Q")
+    d = S.shape[0]
+    if S.dim() != 2 or S.shape[1] != d or Q.dim() != 2 or Q.shape[0] != d:
+        raise ValueError(f"shape mismatch: S {tuple(S.shape)}, Q {tuple(Q.shape)}")
+    p = Q.shape[1]
+    if d % 4 or S.stride(1) != 1 or S.stride(0) % 4 or S.data_ptr() % 16:
+        raise ValueError("S must be row-major with d % 4 == 0 and a 16-byte aligned, %4 stride")
+    if not Q.is_contiguous() or Q.dtype != torch.float32:
+        raise ValueError("Q must be a contiguous float32 tensor (updated in place)")
+    cs = cs.to(device=S.device, dtype=torch.float32).contiguous()
+    if cs.numel() != p:
+        raise ValueError(f"cs must hold p = {p} column scales")
+    Y = out if out is not None else torch.empty((d, p), dtype=torch.float32, device=S.device)
+    code = _lib.DEIG_SWEEP_BF16X6
+    if prepared:
+        code |= _lib.DEIG_SWEEP_PREPARED
+    if round_q:
+        code |= _lib.DEIG_SWEEP_ROUND_Q
+    if fast:
+        code |= _lib.DEIG_SWEEP_FAST
+    L = _lib.lib()
+    with torch.cuda.device(S.device):
+        nbytes = L.deig_sym_apply_workspace(d, p, code)
+        ws = _workspace(S.device, nbytes)
+        rc = L.deig_sym_power_f32(S.data_ptr(), d, S.stride(0), Q.data_ptr(), p, Q.stride(0),
+                                  Y.data_ptr(), Y.stride(0), cs.data_ptr(), int(steps), code,
+                                  ws.data_ptr(), nbytes, _stream(S.device))
+    _lib.check(rc, "deig_sym_power_f32")
     return Y
 
 

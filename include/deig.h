@@ -132,6 +132,20 @@ int deig_sym_apply_f32(const float* S, int64_t d, int64_t lds, const float* Q, i
                        size_t ws_bytes, void* stream);
 size_t deig_sym_apply_workspace(int64_t d, int p, int algo);
 
+/* `steps` sweeps of the solver's power chain (the sweeps between two Rayleigh-Ritz
+ * steps of deig_topk_sym_f32): for i = 0 .. steps-1:  Y = S Q;  Q_j <- cs_j Y_j
+ * for every column with cs_j > 0 (the others keep Q_j).  cs: p floats in device
+ * memory.  Each basis step is fused into the sweep's split-K reduction together
+ * with the next sweep's Q image, as inside the solver, so the time per step is
+ * the solver's cost per sweep.  On return Y = S Q_{steps-1} and Q = Q_steps
+ * (ROUND_Q / FAST: every Q rounded to two bf16 pieces as for deig_sym_apply_f32).
+ * algo: DEIG_SWEEP_BF16X6 / AUTO with the PREPARED / ROUND_Q / FAST flags; the
+ * workspace is deig_sym_apply_workspace's.  Extends the sweep entry point (no
+ * reference counterpart: the reference solves with LAPACK, distributed.py:22-29). */
+int deig_sym_power_f32(const float* S, int64_t d, int64_t lds, float* Q, int p, int64_t ldq,
+                       float* Y, int64_t ldy, const float* cs, int steps, int algo, void* ws,
+                       size_t ws_bytes, void* stream);
+
 /* Top-k eigenpairs of a dense symmetric S (d x d, row-major, lds), ascending.
  * Replaces Node.top_k_eigenvectors  distributed.py:22-29
  * (scipy.linalg.eigh(S, eigvals=(d-k, d-1))[1]  ->  LAPACK dsyevr), plus the

@@ -327,3 +327,38 @@ def test_sym_apply_rejects_bad_p(cuda):
     with pytest.raises(ValueError):
         de.sym_apply(S, torch.ones(64, 24, device=cuda))
 
+
+
+@pytest.mark.parametrize("d,p,mode", [(512, 32, "exact"), (1000, 48, "round_q"), (3072, 32, "fast"),
+                                      (8192, 80, "fast"), (2048, 128, "exact")])
+def test_sym_power_fused_chain(d, p, mode, cuda):
+    """The solver's sweep chain with the power step, the split-K reduction and the
+    next sweep's Q image fused (sweep_finish_kernel) vs the same chain in float64:
+    Y = S Q, Q_j <- cs_j Y_j (cs_j <= 0: column kept)."""
+    import distributed_eigenspaces_amd as de
+    rng = np.random.default_rng(d + p)
+    A = rng.standard_normal((d, d))
+    S = ((A + A.T) / (2 * np.sqrt(d))).astype(np.float32)
+    Q0 = rng.standard_normal((d, p)).astype(np.float32)
+    cs = np.full(p, 0.5, dtype=np.float32)
+    cs[3] = 0.0  # kept column
+    steps = 4
+    St = torch.from_numpy(S).to(cuda)
+    Q = torch.from_numpy(Q0).to(cuda)
+    kw = {"round_q": mode == "round_q", "fast": mode == "fast"}
+    Y = de.sym_power(St, Q, torch.from_numpy(cs), steps, **kw)
+    Qr, S64 = Q0.astype(np.float64), S.astype(np.float64)
+    for _ in range(steps):
+        Yr = S64 @ Qr
+        Qn = Yr * cs
+        Qn[:, cs <= 0] = Qr[:, cs <= 0]
+        Qr = Qn
+    tol = {"exact": 6e-6, "round_q": 5e-5, "fast": 2e-4}[mode]
+    for got, ref in ((Y.cpu().numpy(), Yr), (Q.cpu().numpy(), Qr)):
+        err = np.abs(got - ref).max() / np.abs(ref).max()
+        assert err <= tol, f"sym_power[{mode}] d={d} p={p}: rel err {err:.3e} > {tol:.1e}"
+    if mode != "exact":  # the basis stays rounded to two bf16 pieces, as sym_apply leaves it
+        q = Q.cpu()
+        h = q.to(torch.bfloat16).float()
+        m = (q - h).to(torch.bfloat16).float()
+        assert torch.equal(h + m, q)
