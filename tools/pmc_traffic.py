@@ -21,11 +21,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def source_sha256():
-    """Hash of the covariance kernel sources the measurement describes (bench.py
-    reports the traffic only while the sources still hash the same)."""
+    """Hash of the covariance kernel source the measurement describes (bench.py
+    reports the traffic only while it still hashes the same).  syrk_split.hip holds
+    every kernel of the op (split, SYRK, reduce, diagonal correction); the shared
+    header only declares other modules' entry points, so it is not hashed."""
     h = hashlib.sha256()
-    for f in ("syrk_split.hip", "deig_internal.hpp"):
-        h.update(open(os.path.join(ROOT, "distributed_eigenspaces_amd", "csrc", f), "rb").read())
+    h.update(open(os.path.join(ROOT, "distributed_eigenspaces_amd", "csrc", "syrk_split.hip"),
+                  "rb").read())
     return h.hexdigest()
 
 KERNELS = ["split_kernel", "syrks_kernel", "syrks_reduce_kernel", "diag_corr_kernel",
