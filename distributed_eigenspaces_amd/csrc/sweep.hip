@@ -1002,7 +1002,11 @@ int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, i
       default: launch_v1<8>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
     }
   } else {
-    const bool v3 = sweep_version() == 3 || (sweep_version() == 0 && nb > 5);
+    // default: v3 above p = 80 (v2's rings spill) and for the early-sweep mode from
+    // p = 64 (no split in the sweep, so the LDS-shared Q pays; rocprof, d = 8192:
+    // p = 80 50.6 vs 55.3 us, p = 64 47.2 vs 48.3; p = 32 at d = 3072 11.4 vs 11.0,
+    // profiles/r02l_sweep_v3pre.log; v2 stays faster with the split)
+    const bool v3 = sweep_version() == 3 || (sweep_version() == 0 && (nb > 5 || (pre && nb >= 4)));
     if (pre)
       launch_image<2, true>(v3, nb, grid, st, reinterpret_cast<const f32x4*>(w.SH), d, w.QS, Y,
                             ldy, alpha, w.part);
