@@ -936,9 +936,15 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
   float* corr = reinterpret_cast<float*>(base + L.off_corr);
   unsigned char* xp = reinterpret_cast<unsigned char*>(base + L.off_xp);
 
-  // Two-level fp32 summation: accumulators are added into a per-block slab
-  // every flush_rows rows (DEIG_SYRK_FLUSH_ROWS overrides, for A/B runs).
+  // Two-level fp32 summation: accumulators are added into a per-block slab every
+  // flush_rows rows.  The error bound ~ (flush_rows / 32 + n / flush_rows) eps is
+  // smallest at flush_rows ~ sqrt(32 n): 2^floor(log2 sqrt(32 n)) within [4096, 16384]
+  // (config 3, n = 2^21: 8192 - vs 4096 the op ran 337.6 -> 331.1 ms with sampled
+  // error 5.0e-7 -> 4.7e-7, profiles/r02l_syrk_flush.log; fewer flushes, each a
+  // read-add-write of the block's 256 KiB slab beside stalled MFMAs).
+  // DEIG_SYRK_FLUSH_ROWS overrides, for A/B runs.
   int64_t flush_rows = 4096;
+  while (flush_rows < 16384 && (flush_rows * 2) * (flush_rows * 2) <= 32 * n) flush_rows *= 2;
   if (const char* v = getenv("DEIG_SYRK_FLUSH_ROWS")) flush_rows = atoll(v);
   if (flush_rows < 32) flush_rows = 32;
   if (flush_rows > (int64_t(1) << 30)) flush_rows = int64_t(1) << 30;

@@ -25,3 +25,17 @@ r["measured"] = f"profile round {tag}, {time.strftime('%Y-%m-%d')}"
 json.dump(r, open(p, "w"), indent=1)
 PY
 ls $OUT/trace
+# config 2 (2^20 x 3072, fused split): its own PMC record for bench.py --config c2
+timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch_c2 -o p -- \
+  python3 $R/tools/run_syrk_once.py 1048576 3072 > $OUT/fetch_c2.log 2>&1 || { echo "c2 fetch pass failed"; tail $OUT/fetch_c2.log; exit 1; }
+timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write_c2 -o p -- \
+  python3 $R/tools/run_syrk_once.py 1048576 3072 > $OUT/write_c2.log 2>&1 || { echo "c2 write pass failed"; tail $OUT/write_c2.log; exit 1; }
+python3 $R/tools/pmc_traffic.py $OUT/fetch_c2 $OUT/write_c2 $OUT/pmc_syrk_c2_split3.json 1048576 3072 \
+  "covariance split3, fused split (syrks_kernel<..., true> + syrks_reduce_kernel + diag_corr_kernel)" > /dev/null \
+  && python3 - $OUT/pmc_syrk_c2_split3.json $TAG <<'PY'
+import json, sys, time
+p, tag = sys.argv[1:3]
+r = json.load(open(p))
+r["measured"] = f"profile round {tag}, {time.strftime('%Y-%m-%d')}"
+json.dump(r, open(p, "w"), indent=1)
+PY
