@@ -568,13 +568,31 @@ __device__ __forceinline__ void sw_dma16(const __amdgpu_buffer_rsrc_t rsrc, int 
                : "memory", "m0");
 }
 
-template <int NB, int NP, int D, int OCC = 1, bool PRE = false>
+// body(integral_constant<B>, g + B) for B = B0 .. D - 1 (tail: only while g + B < c1).
+template <int B, int D>
+struct UnrollBodies {
+  template <class F>
+  static __device__ __forceinline__ void run(F& f, int64_t g, int64_t c1, bool tail) {
+    if (!tail || g + B < c1) f(std::integral_constant<int, B>{}, g + B);
+    UnrollBodies<B + 1, D>::run(f, g, c1, tail);
+  }
+};
+template <int D>
+struct UnrollBodies<D, D> {
+  template <class F>
+  static __device__ __forceinline__ void run(F&, int64_t, int64_t, bool) {}
+};
+
+// MBW: 16-row m-blocks per wave (4: 64 rows, one image row block; 2: half of one,
+// so a block covers 128 rows and the grid needs half the split-K slices).
+template <int NB, int NP, int D, int OCC = 1, bool PRE = false, int MBW = 4>
 __global__ __launch_bounds__(256, OCC) void sweep3_kernel(const f32x4* __restrict__ SI, int64_t d,
                                                         const u32x4* __restrict__ QS,
                                                         int64_t ngrp, float* __restrict__ Y,
                                                         int64_t ldy, float alpha,
                                                         float* __restrict__ part) {
-  constexpr int MB = 4;
+  constexpr int MB = MBW;
+  static_assert(MB == 2 || MB == 4, "m-blocks per wave");
   constexpr int U = NP * NB;         // 1-KiB Q pieces per k-group
   constexpr int ND = (U + 3) / 4;    // DMAs per wave per group (tail pieces repeated)
   constexpr int SLOT = U * 1024;     // bytes per ring slot
@@ -584,12 +602,12 @@ __global__ __launch_bounds__(256, OCC) void sweep3_kernel(const f32x4* __restric
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, gq = lane >> 4;
-  const int bx = (int)cdiv(d, SI_BR);
+  const int bx = (int)cdiv(d, 4 * 16 * MB);
   const int ks = (int)(gridDim.x / bx);
   const int lid = xcd_logical(blockIdx.x, gridDim.x);
   const int sl = lid / bx;
-  const int64_t rb = (int64_t)(lid - sl * bx) * (SI_BR / SI_RB) + wave;
-  const int64_t row0 = rb * SI_RB;
+  const int64_t rb = (int64_t)(lid - sl * bx) * 4 + wave;  // this wave's 16 MB rows
+  const int64_t row0 = rb * 16 * MB;
   const int64_t c0 = ngrp * sl / ks, c1 = ngrp * (sl + 1) / ks;
 
   f32x4 acc[MB][NB];
@@ -600,7 +618,8 @@ __global__ __launch_bounds__(256, OCC) void sweep3_kernel(const f32x4* __restric
 
   const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<u32x4*>(QS), 0, (int)(ngrp * U * 1024), 0x00020000);
-  const f32x4* sw = SI + rb * ngrp * (MB * 2 * 64) + lane;
+  // image row block row0 / 64, starting at its m-block (row0 % 64) / 16
+  const f32x4* sw = SI + (row0 / SI_RB) * ngrp * (4 * 2 * 64) + ((row0 % SI_RB) / 16) * 2 * 64 + lane;
   f32x4 sr[D][MB][2];
   auto load = [&](int b, int64_t g) {
     // Q pieces first: the compiler's wait for this group's S registers then
@@ -611,7 +630,7 @@ __global__ __launch_bounds__(256, OCC) void sweep3_kernel(const f32x4* __restric
       const int u = wave + 4 * i < U ? wave + 4 * i : U - 1;
       sw_dma16(qrs, (int)((g * U + u) * 1024) + lane * 16, slot + u * 1024);
     }
-    const f32x4* sg = sw + g * (MB * 2 * 64);
+    const f32x4* sg = sw + g * (4 * 2 * 64);
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
@@ -654,17 +673,11 @@ __global__ __launch_bounds__(256, OCC) void sweep3_kernel(const f32x4* __restric
 #pragma unroll
     for (int b = 0; b < D; ++b) load(b, c0 + b < c1 ? c0 + b : c1 - 1);
     __builtin_amdgcn_sched_barrier(0);
+    // D bodies per trip (register set B takes groups c0 + B mod D), then the
+    // fewer than D groups left
     int64_t g = c0;
-    for (; g + D <= c1; g += D) {
-      body(std::integral_constant<int, 0>{}, g);
-      body(std::integral_constant<int, 1>{}, g + 1);
-      if constexpr (D > 2) body(std::integral_constant<int, 2>{}, g + 2);
-      if constexpr (D > 3) body(std::integral_constant<int, 3>{}, g + 3);
-    }
-    if (g < c1) body(std::integral_constant<int, 0>{}, g);
-    if (g + 1 < c1) body(std::integral_constant<int, 1>{}, g + 1);
-    if constexpr (D > 3)
-      if (g + 2 < c1) body(std::integral_constant<int, 2>{}, g + 2);
+    for (; g + D <= c1; g += D) UnrollBodies<0, D>::run(body, g, c1, false);
+    UnrollBodies<0, D - 1>::run(body, g, c1, true);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the block's LDS
 
@@ -812,6 +825,35 @@ int sweep_ks(int64_t d) {
   return (int)ks;
 }
 
+// m-blocks per wave of the v3 kernel: 2 for the early-sweep mode up to p = 80
+// (128-row blocks: half the split-K slices, so half the slab bytes the sweep writes
+// and its epilogue reads; rocprof d = 8192: p = 80 47.2 vs 50.6 us, p = 64 45.4 vs
+// 47.9, per sweep in the chain 52.4 vs 58.0), else 4 (p = 128: 272 vs 249 us per
+// sweep - there the Q fragment reuse of 64-row waves wins; with the split in the
+// sweep no gain either).  Ring depths 5-8 measured the same as 3
+// (profiles/r02n_sweep_mb.log).  DEIG_SWEEP_MB=2|4 overrides.
+int sweep_mb(bool pre, int nb) {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DEIG_SWEEP_MB");
+    v = (e && (atoi(e) == 2 || atoi(e) == 4)) ? atoi(e) : 0;
+  }
+  if (v) return v;
+  return (pre && nb <= 5) ? 2 : 4;
+}
+
+// Split-K slices of a v3 launch with mb m-blocks per wave (rows per block 64 mb).
+int sweep_ks_mb(int64_t d, int mb) {
+  if (mb == 4) return sweep_ks(d);
+  const int64_t bx = cdiv(d, 64 * mb), nsteps = cdiv(d, SW_KS);
+  int64_t ks = cdiv((int64_t)num_cus() * sweep_bpc(), bx);
+  const int64_t cap = nsteps / 4 > 1 ? nsteps / 4 : 1;
+  if (ks > cap) ks = cap;
+  if (ks < 1) ks = 1;
+  const int64_t kmax = sweep_ks(d);  // the workspace holds sweep_ks(d) slabs
+  return (int)(ks < kmax ? ks : kmax);
+}
+
 // Q image: 3 bf16 pieces per value
 size_t qs_bytes(int64_t d, int p) { return (size_t)cdiv(d, SW_KS) * SW_KS * p * 6; }
 
@@ -871,6 +913,36 @@ void launch_v3(dim3 grid, hipStream_t st, const f32x4* SI, int64_t d, const u32x
                int64_t ldy, float alpha, float* part) {
   static const int de = getenv("DEIG_SWEEP_DEPTH") ? atoi(getenv("DEIG_SWEEP_DEPTH")) : 3;
   const int64_t ng = si_groups(d);
+  if (sweep_mb(PRE, NB) == 2) {
+    if constexpr (9 * NP * NB * 1024 <= 160 * 1024) {
+      if (de == 8) {
+        hipLaunchKernelGGL((sweep3_kernel<NB, NP, 8, 1, PRE, 2>), grid, dim3(256), 0, st, SI, d,
+                           QS, ng, Y, ldy, alpha, part);
+        return;
+      }
+    }
+    if constexpr (7 * NP * NB * 1024 <= 160 * 1024) {
+      if (de == 6) {
+        hipLaunchKernelGGL((sweep3_kernel<NB, NP, 6, 1, PRE, 2>), grid, dim3(256), 0, st, SI, d,
+                           QS, ng, Y, ldy, alpha, part);
+        return;
+      }
+    }
+    if constexpr (6 * NP * NB * 1024 <= 160 * 1024) {
+      if (de == 5) {
+        hipLaunchKernelGGL((sweep3_kernel<NB, NP, 5, 1, PRE, 2>), grid, dim3(256), 0, st, SI, d,
+                           QS, ng, Y, ldy, alpha, part);
+        return;
+      }
+    }
+    if (de == 4)
+      hipLaunchKernelGGL((sweep3_kernel<NB, NP, 4, 1, PRE, 2>), grid, dim3(256), 0, st, SI, d, QS,
+                         ng, Y, ldy, alpha, part);
+    else
+      hipLaunchKernelGGL((sweep3_kernel<NB, NP, 3, 1, PRE, 2>), grid, dim3(256), 0, st, SI, d, QS,
+                         ng, Y, ldy, alpha, part);
+    return;
+  }
   if (de == 4)
     hipLaunchKernelGGL((sweep3_kernel<NB, NP, 4, 1, PRE>), grid, dim3(256), 0, st, SI, d, QS, ng,
                        Y, ldy, alpha, part);
@@ -988,8 +1060,10 @@ int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, i
                          nb, ngrp, w.QS);
     DEIG_HIP_CHECK(hipGetLastError());
   }
-  const int ks = sweep_ks(d);
-  const dim3 grid((unsigned)(cdiv(d, SW_ROWS) * ks));
+  const bool v3 = sweep_version() == 3 || (sweep_version() == 0 && (nb > 5 || (pre && nb >= 4)));
+  const int mbw = (sweep_version() != 1 && v3) ? sweep_mb(pre, nb) : 4;
+  const int ks = sweep_ks_mb(d, mbw);
+  const dim3 grid((unsigned)(cdiv(d, mbw == 4 ? SW_ROWS : 64 * mbw) * ks));
   if (sweep_version() == 1) {
     switch (nb) {
       case 1: launch_v1<1>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
@@ -1002,11 +1076,10 @@ int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, i
       default: launch_v1<8>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
     }
   } else {
-    // default: v3 above p = 80 (v2's rings spill) and for the early-sweep mode from
-    // p = 64 (no split in the sweep, so the LDS-shared Q pays; rocprof, d = 8192:
-    // p = 80 50.6 vs 55.3 us, p = 64 47.2 vs 48.3; p = 32 at d = 3072 11.4 vs 11.0,
-    // profiles/r02l_sweep_v3pre.log; v2 stays faster with the split)
-    const bool v3 = sweep_version() == 3 || (sweep_version() == 0 && (nb > 5 || (pre && nb >= 4)));
+    // v3 (above): the default above p = 80 (v2's rings spill) and for the early-sweep
+    // mode from p = 64 (no split in the sweep, so the LDS-shared Q pays; rocprof,
+    // d = 8192: p = 80 50.6 vs 55.3 us, p = 64 47.2 vs 48.3; p = 32 at d = 3072 11.4
+    // vs 11.0, profiles/r02l_sweep_v3pre.log; v2 stays faster with the split)
     if (pre)
       launch_image<2, true>(v3, nb, grid, st, reinterpret_cast<const f32x4*>(w.SH), d, w.QS, Y,
                             ldy, alpha, w.part);
