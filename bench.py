@@ -273,8 +273,15 @@ def sweep_roofline(de, S: torch.Tensor, p: int, stream) -> dict:
                                                    round_q=rq, fast=fa), 3, stream) / nst
             out[algo]["in_solver_chain_us"] = cms * 1e3
             out[algo]["in_solver_chain_hbm_frac"] = byt / (cms * 1e-3) / HBM_PEAK
-    out["kernel"] = ("us: split_q_kernel + sweep2_kernel (p <= 80) / sweep3_kernel (p > 80) (+ "
-                     "sweep_reduce_kernel), one standalone product; in_solver_chain_us: sweep kernel "
+            # the sweep kernel alone (DEIG_SWEEP_KERNEL_ONLY: on the Q image the last
+            # call left, no split of Q, no split-K reduction)
+            de.sym_apply(S, Q, out=Y, prepared=True, round_q=rq, fast=fa)
+            kms = time_events(lambda: de.sym_apply(S, Q, out=Y, prepared=True, round_q=rq,
+                                                   fast=fa, kernel_only=True), 20, stream)
+            out[algo]["kernel_us"] = kms * 1e3
+            out[algo]["kernel_hbm_frac"] = byt / (kms * 1e-3) / HBM_PEAK
+    out["kernel"] = ("us: split_q_kernel + sweep2_kernel / sweep3_kernel (+ sweep_reduce_kernel), "
+                     "one standalone product; kernel_us: the sweep kernel alone; in_solver_chain_us: sweep kernel "
                      "+ sweep_finish_kernel (split-K reduction, power step and next Q image fused), "
                      "per sweep of a 10-sweep chain; on the S images (sweep_prepare_kernel, once per solve): "
                      "bf16x3 = 3 bf16 MFMA 16x16x32 products of the prepared two-piece S image and "

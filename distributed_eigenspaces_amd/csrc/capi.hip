@@ -576,7 +576,7 @@ int deig_sym_power_f32(const float* S, int64_t d, int64_t lds, float* Q, int p, 
 }
 
 size_t deig_sym_apply_workspace(int64_t d, int p, int algo) {
-  algo &= ~(DEIG_SWEEP_PREPARED | DEIG_SWEEP_ROUND_Q | DEIG_SWEEP_FAST);
+  algo &= ~(DEIG_SWEEP_PREPARED | DEIG_SWEEP_ROUND_Q | DEIG_SWEEP_FAST | DEIG_SWEEP_KERNEL_ONLY);
   if (algo == DEIG_SWEEP_FP32) return skinny_workspace_bytes(d, p, d);
   return sweep_workspace_bytes(d, p);
 }
@@ -589,10 +589,11 @@ int deig_sym_apply_f32(const float* S, int64_t d, int64_t lds, const float* Q, i
     return skinny_launch(true, S, lds, Q, ldq, Y, ldy, d, p, d, alpha, 0.f,
                          static_cast<float*>(ws), ws_bytes, (hipStream_t)stream);
   const bool prepared = (algo & DEIG_SWEEP_PREPARED) != 0;
+  const bool kernel_only = (algo & DEIG_SWEEP_KERNEL_ONLY) != 0;
   const int smode = (algo & DEIG_SWEEP_FAST)      ? kSweepFast
                     : (algo & DEIG_SWEEP_ROUND_Q) ? kSweepRoundQ
                                                   : kSweepExact;
-  algo &= ~(DEIG_SWEEP_PREPARED | DEIG_SWEEP_ROUND_Q | DEIG_SWEEP_FAST);
+  algo &= ~(DEIG_SWEEP_PREPARED | DEIG_SWEEP_ROUND_Q | DEIG_SWEEP_FAST | DEIG_SWEEP_KERNEL_ONLY);
   if (algo != DEIG_SWEEP_AUTO && algo != DEIG_SWEEP_BF16X6)
     return fail(DEIG_EINVAL, "sym_apply: unknown algorithm %d", algo);
   if (!prepared) {
@@ -600,7 +601,7 @@ int deig_sym_apply_f32(const float* S, int64_t d, int64_t lds, const float* Q, i
     if (rc) return rc;
   }
   return sweep_apply(S, d, lds, Q, p, ldq, Y, ldy, alpha, ws, ws_bytes, (hipStream_t)stream,
-                     smode);
+                     smode, nullptr, kernel_only, kernel_only);
 }
 
 size_t deig_oja_workspace(int64_t b, int64_t d, int k) { return oja_workspace_bytes(b, d, k); }

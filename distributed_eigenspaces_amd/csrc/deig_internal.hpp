@@ -127,7 +127,8 @@ struct SweepStep {
 };
 int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
                 float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st,
-                int mode = kSweepExact, const SweepStep* step = nullptr, bool q_ready = false);
+                int mode = kSweepExact, const SweepStep* step = nullptr, bool q_ready = false,
+                bool kernel_only = false);  // kernel_only: no split-K reduction (measurement)
 
 // Rayleigh-Ritz pieces (rr.hip).
 struct RRBuffers {

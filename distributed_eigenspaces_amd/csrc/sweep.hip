@@ -1034,7 +1034,7 @@ int sweep_round_pieces() {
 
 int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
                 float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st,
-                int mode, const SweepStep* step, bool q_ready) {
+                int mode, const SweepStep* step, bool q_ready, bool kernel_only) {
   const bool round_q = mode >= 1;
   DEIG_REQUIRE(d >= 1 && p >= 16 && p <= 128 && p % 16 == 0,
                "sweep: need d >= 1 and p in {16, 32, ..., 128} (p=%d)", p);
@@ -1089,6 +1089,7 @@ int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, i
       launch_image<3>(v3, nb, grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part);
   }
   DEIG_HIP_CHECK(hipGetLastError());
+  if (kernel_only) return DEIG_OK;
   if (step) {
     DEIG_REQUIRE(ldy % 4 == 0 && aligned16(Y) && step->ldq % 4 == 0 && aligned16(step->Q) &&
                      (step->kind == 1 || step->kind == 2),

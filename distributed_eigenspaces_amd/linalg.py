@@ -437,7 +437,8 @@ def oja_steps(X: torch.Tensor, V: torch.Tensor, eta: float, batch: int,
 # ---------------------------------------------------------------- sweep
 def sym_apply(S: torch.Tensor, Q: torch.Tensor, algo: str = "auto", alpha: float = 1.0,
               out: torch.Tensor | None = None, prepared: bool = False,
-              round_q: bool = False, fast: bool = False) -> torch.Tensor:
+              round_q: bool = False, fast: bool = False,
+              kernel_only: bool = False) -> torch.Tensor:
     """Y = alpha * S Q for symmetric S (d x d) and Q (d x p, p % 16 == 0, p <= 128):
     one subspace-iteration sweep of ``topk_eigh`` (include/deig.h DEIG_SWEEP_*):
     algo "bf16x6" (default via "auto") or "fp32".  ``prepared=True`` (bf16x6) reuses
@@ -447,7 +448,9 @@ def sym_apply(S: torch.Tensor, Q: torch.Tensor, algo: str = "auto", alpha: float
     modified in place) is rounded to its two leading bf16 pieces and Y = alpha S Q'
     is formed from five bf16 products.  ``fast=True`` (implies round_q; the solver's
     early-sweep mode, DEIG_SWEEP_FAST): S is also taken as its two leading bf16
-    pieces, three products, ~2^-16 relative."""
+    pieces, three products, ~2^-16 relative.  ``kernel_only=True`` (measurement,
+    DEIG_SWEEP_KERNEL_ONLY): only the sweep kernel runs, on the Q image the previous
+    call in this stream's workspace left; ``out`` is not written."""
     round_q = round_q or fast
     if algo not in _lib.SWEEP_ALGOS:
         raise ValueError(f"algo must be one of {sorted(_lib.SWEEP_ALGOS)}, got {algo!r}")
@@ -472,6 +475,10 @@ def sym_apply(S: torch.Tensor, Q: torch.Tensor, algo: str = "auto", alpha: float
         code |= _lib.DEIG_SWEEP_ROUND_Q
     if fast:
         code |= _lib.DEIG_SWEEP_FAST
+    if kernel_only:
+        if code & 0xff == _lib.DEIG_SWEEP_FP32:
+            raise ValueError("kernel_only needs algo bf16x6/auto")
+        code |= _lib.DEIG_SWEEP_KERNEL_ONLY | _lib.DEIG_SWEEP_PREPARED
     L = _lib.lib()
     with torch.cuda.device(S.device):
         nbytes = L.deig_sym_apply_workspace(d, p, code)

@@ -123,6 +123,11 @@ int deig_default_subspace(int64_t d, int k);
  * relative (S' rounding 2^-17, dropped m m 2^-18).  deig_topk_sym_f32 uses it while
  * its residual is above 1e-3, ROUND_Q down to 1e-4, the exact product below. */
 #define DEIG_SWEEP_FAST 0x400
+/* OR-ed into the algorithm of deig_sym_apply_f32 (BF16X6 only; measurement):
+ * launch the sweep kernel alone on the Q image that the previous call with the
+ * same workspace, d, p and mode left - no split of Q, no split-K reduction, Y is
+ * not written.  Timing such calls gives the sweep kernel's own duration. */
+#define DEIG_SWEEP_KERNEL_ONLY 0x800
 
 /* One subspace-iteration sweep Y = alpha * S Q  (S symmetric d x d row-major, lds;
  * Q d x p row-major, ldq; Y d x p row-major, ldy; p % 16 == 0, 16 <= p <= 128).
