@@ -259,9 +259,26 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
       (rc = sweep_prepare(op.S, d, op.lds, p, w.sweep_ws, w.sweep_bytes, st)))
     return rc;
   float lam_h[kMaxP];
+  float res_h[kMaxP + 1];  // per-column residuals of the last RR (descending Ritz order)
   int it = 0;  // sweeps done (both stages)
   float last = 3.4e38f;
   bool converged = false;
+  // Stage 1 may end as soon as the dominant pairs that stage 2 deflates are
+  // converged (their own residuals <= tol), instead of waiting for every column:
+  // with theta_0 ~ 10^4 theta_k (uncentered data) the Chebyshev filter of stage 1
+  // is held to degree 1 by the dominant direction's growth bound, so its later
+  // cycles are one sweep per Rayleigh-Ritz step.  DEIG_DEFLATE_EARLY=0: off.
+  static const bool deflate_on = !(getenv("DEIG_DEFLATE") && getenv("DEIG_DEFLATE")[0] == '0');
+  static const bool deflate_early =
+      !(getenv("DEIG_DEFLATE_EARLY") && getenv("DEIG_DEFLATE_EARLY")[0] == '0');
+  const bool can_deflate = deflate_on && !op.implicit && w.sweep_ws && sweep_version() != 1 && k >= 2;
+  auto dominant = [&](int kk) {  // pairs stage 2 would deflate (0: none)
+    if (!(lam_h[kk - 1] > 0.f && lam_h[0] >= kDeflateRatio * lam_h[kk - 1])) return 0;
+    int r = 0;
+    while (r < kk - 1 && r < kMaxDeflate && lam_h[r] >= kDeflateRatio * lam_h[kk - 1]) ++r;
+    return r;
+  };
+  bool early = false;
   // Sweeps round Q to two bf16 pieces (five products instead of six, sweep.hip
   // split_q_kernel) while the residual is above round_until: the rounding puts
   // ~4e-6 relative noise into the basis each sweep, harmless while the Ritz
@@ -348,9 +365,10 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
       if ((rc2 = rr_small_launch(w.rr, p, st, jcap))) return rc2;
       if ((rc2 = rr_update_launch(w.rr, d, p, kc, V, ldv, evals, st))) return rc2;
       DEIG_HIP_CHECK(
-          hipMemcpyAsync(&last, w.rr.resid + kc, sizeof(float), hipMemcpyDeviceToHost, st));
+          hipMemcpyAsync(res_h, w.rr.resid, sizeof(float) * (kc + 1), hipMemcpyDeviceToHost, st));
       DEIG_HIP_CHECK(hipMemcpyAsync(lam_h, w.rr.lam, sizeof(float) * p, hipMemcpyDeviceToHost, st));
       DEIG_HIP_CHECK(hipStreamSynchronize(st));
+      last = res_h[kc];
       ++nrr;
       if (debug) {
         int inf[9] = {0};
@@ -367,6 +385,15 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
       if (last <= tol) {
         converged = true;
         return DEIG_OK;
+      }
+      if (kc == k && can_deflate && deflate_early && last == last) {
+        const int r = dominant(k);
+        bool ok = r >= 1;
+        for (int j = 0; j < r && ok; ++j) ok = res_h[j] <= tol;
+        if (ok) {
+          early = true;
+          return DEIG_OK;
+        }
       }
       // Stagnation: no 10% improvement over the best residual for 4 Rayleigh-Ritz
       // steps in a row.  It counts as convergence only at the fp32 floor (residual
@@ -403,11 +430,8 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
   // remaining k - r pairs are iterated again from their current values (warm
   // start), with the residual now relative to theta_r.  V_D stays in the last r
   // columns of V (ascending order), which the second stage does not touch.
-  static const bool deflate_on = !(getenv("DEIG_DEFLATE") && getenv("DEIG_DEFLATE")[0] == '0');
-  if (deflate_on && converged && !op.implicit && w.sweep_ws && sweep_version() != 1 && k >= 2 &&
-      lam_h[k - 1] > 0.f && lam_h[0] >= kDeflateRatio * lam_h[k - 1]) {
-    int r = 0;
-    while (r < k - 1 && r < kMaxDeflate && lam_h[r] >= kDeflateRatio * lam_h[k - 1]) ++r;
+  if (can_deflate && (converged || early) && dominant(k) >= 1) {
+    const int r = dominant(k);
     const int kc = k - r;
     const float* Vd = V + (int64_t)kc * ldv;
     if ((rc = sweep_prepare(op.S, d, op.lds, p, w.sweep_ws, w.sweep_bytes, st, Vd, ldv,
@@ -417,8 +441,8 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
     rc = iterate(kc);
     if (!rc) rc = deflate_orth_launch(V, ldv, d, kc, r, st);
     if (debug)
-      fprintf(stderr, "[deig] deflated %d dominant pair(s): stage 2 resid %.3e after %d sweeps\n",
-              r, last, it);
+      fprintf(stderr, "[deig] deflated %d dominant pair(s)%s: stage 2 resid %.3e after %d sweeps\n",
+              r, early ? " (early)" : "", last, it);
     if (rc) {
       if (sweeps_out) *sweeps_out = it;
       if (resid_out) *resid_out = last;
