@@ -187,6 +187,10 @@ bool fused_steps(const Operator& op, const SolverWs& w) { return !op.implicit &&
 // Only used once resid <= kChebAbove: before that the Ritz values are too rough
 // to place the interval, and plain power steps run.
 constexpr float kChebAbove = 1e-2f;
+float cheb_above() {  // DEIG_CHEB_ABOVE overrides (A/B)
+  static const float v = getenv("DEIG_CHEB_ABOVE") ? (float)atof(getenv("DEIG_CHEB_ABOVE")) : kChebAbove;
+  return v;
+}
 constexpr double kChebGmax = 1e4;
 constexpr int kChebMaxDeg = 16;
 
@@ -197,7 +201,7 @@ struct ChebPlan {
 };
 
 bool cheb_plan(const float* lam, int k, int p, float resid, float tol, ChebPlan* pl) {
-  if (!(resid <= kChebAbove) || !(resid > 0)) return false;
+  if (!(resid <= cheb_above()) || !(resid > 0)) return false;
   const double gmax = fmin(kChebGmax, fmax(10.0, 1.0 / (double)resid));
   const double a = 0.0;
   double c = lam[p - 1];
