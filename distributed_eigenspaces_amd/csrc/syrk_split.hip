@@ -389,112 +389,6 @@ struct Acc<16> {
     }
   }
 
-  // Fused split (variant 163): K-tile t's MFMAs (KT = 2: one 32-deep step) with
-  // the split of this wave's region R of K-tile t + 1 woven in.  Register budget
-  // (2 waves/SIMD: 256 each, 176 held by accumulators and operands) allows 24 live
-  // fp32 inputs, so the split runs in the order the slices overwrite the staged
-  // rows: half h = 0 of the features writes hi into rows 0-1 and lo into rows 4-5,
-  // so rows {0, 1, 4, 5} (both halves) and the h = 0 halves of rows {2, 3, 6, 7}
-  // are read first (after block 1), h = 0 is split beside blocks 3-4, the h = 1
-  // halves of rows {2, 3, 6, 7} are read at block 5 and split beside blocks 6-7.
-  // The wave's LDS queue is in order, so no write overtakes an earlier read.
-  template <bool SQ>
-  __device__ __forceinline__ void split_group(unsigned char* R, int lane, int h, int e,
-                                              const f32x2 (&v)[8], float* sq) {
-    u32x4 hv, lv;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const float x0 = v[2 * p][e], x1 = v[2 * p + 1][e];
-      const uint32_t hh = cvt2(x0, x1);
-      const float r0 = x0 - lo_f(hh), r1 = x1 - hi_f(hh);
-      hv[p] = hh;
-      lv[p] = cvt2(r0, r1);
-      if (SQ) sq[2 * h + e] = fmaf(r0, r0, fmaf(r1, r1, sq[2 * h + e]));
-    }
-    const int f = 128 * h + 2 * lane + e;
-    *reinterpret_cast<u32x4*>(R + f * 16) = hv;
-    *reinterpret_cast<u32x4*>(R + SLICE_B + f * 16) = lv;
-  }
-
-  __device__ __forceinline__ void mfma_block(int mb, const bf16x8& ahi, const bf16x8& alo,
-                                             const bf16x8 (&bhi)[4], const bf16x8 (&blo)[4]) {
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb)
-      a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi[nb], a[mb][nb], 0, 0, 0);
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb)
-      a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, blo[nb], a[mb][nb], 0, 0, 0);
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb)
-      a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bhi[nb], a[mb][nb], 0, 0, 0);
-  }
-
-  template <bool SQ>
-  __device__ __forceinline__ void mma_fx(const unsigned char* A, const unsigned char* B, int wi,
-                                         int wj, int lane, unsigned char* R, float* sq) {
-    const int c = lane & 15, g = lane >> 4;
-    const unsigned char* ph = A + ((g * 2) * BT + 128 * wi + c) * 16;
-    const unsigned char* qh = B + ((g * 2) * BT + 64 * wj + c) * 16;
-    bf16x8 bhi[4], blo[4], ahi[2], alo[2];
-    ahi[0] = *reinterpret_cast<const bf16x8*>(ph);
-    alo[0] = *reinterpret_cast<const bf16x8*>(ph + BT * 16);
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {
-      bhi[nb] = *reinterpret_cast<const bf16x8*>(qh + (16 * nb) * 16);
-      blo[nb] = *reinterpret_cast<const bf16x8*>(qh + (BT + 16 * nb) * 16);
-    }
-    // region 1: blocks 0-1 (the DMAs of K-tile t + 1 are in flight)
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb) {
-      ahi[(mb + 1) & 1] = *reinterpret_cast<const bf16x8*>(ph + (16 * (mb + 1)) * 16);
-      alo[(mb + 1) & 1] = *reinterpret_cast<const bf16x8*>(ph + (BT + 16 * (mb + 1)) * 16);
-      mfma_block(mb, ahi[mb & 1], alo[mb & 1], bhi, blo);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x100, 10, 0);
-    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
-    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
-    wait_vm<0>();  // this wave's DMAs of K-tile t + 1 (its own region) landed
-    // region 2: blocks 2-7 with the split
-    f32x2 v0[8], v1[8];  // h = 0 rows 0-7; h = 1 rows 0, 1, 4, 5 then 2, 3, 6, 7
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      v0[r] = *reinterpret_cast<const f32x2*>(R + r * 1024 + 8 * lane);
-      if ((r & 2) == 0) v1[r] = *reinterpret_cast<const f32x2*>(R + r * 1024 + 512 + 8 * lane);
-    }
-#pragma unroll
-    for (int mb = 2; mb < 8; ++mb) {
-      if (mb + 1 < 8) {
-        ahi[(mb + 1) & 1] = *reinterpret_cast<const bf16x8*>(ph + (16 * (mb + 1)) * 16);
-        alo[(mb + 1) & 1] = *reinterpret_cast<const bf16x8*>(ph + (BT + 16 * (mb + 1)) * 16);
-      }
-      if (mb == 5) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r)
-          if ((r & 2) != 0) v1[r] = *reinterpret_cast<const f32x2*>(R + r * 1024 + 512 + 8 * lane);
-      }
-      mfma_block(mb, ahi[mb & 1], alo[mb & 1], bhi, blo);
-      if (mb == 3 || mb == 4) split_group<SQ>(R, lane, 0, mb - 3, v0, sq);
-      if (mb == 6 || mb == 7) split_group<SQ>(R, lane, 1, mb - 6, v1, sq);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-#pragma unroll
-    for (int mb = 2; mb < 8; ++mb) {
-      if (mb + 1 < 8) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      if (mb == 5) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-      if (mb == 2 || mb == 5) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, SQ ? 3 : 2, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
-      }
-    }
-  }
 };
 
 constexpr int NQUAD = 32;
