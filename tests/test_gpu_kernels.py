@@ -362,3 +362,30 @@ def test_sym_power_fused_chain(d, p, mode, cuda):
         h = q.to(torch.bfloat16).float()
         m = (q - h).to(torch.bfloat16).float()
         assert torch.equal(h + m, q)
+
+
+@pytest.mark.parametrize("d", [4096, 4100])
+def test_syrk_split3_variant_boundary(d, cuda):
+    """Either side of the default's width switch (fused split up to d = 4096, the
+    split pass above), ragged n: both vs float64."""
+    rng = np.random.default_rng(d)
+    X = (rng.standard_normal((2085, d)) + 0.25).astype(np.float32)
+    _syrk_check(X, cuda, rel=_split3_tol(2085), algo="split3")
+
+
+def test_sym_apply_kernel_only_leaves_y(cuda):
+    """DEIG_SWEEP_KERNEL_ONLY (measurement): the sweep kernel alone - Y untouched,
+    and a following full call still returns S Q."""
+    import distributed_eigenspaces_amd as de
+    rng = np.random.default_rng(7)
+    d, p = 1024, 48
+    A = rng.standard_normal((d, d))
+    S = torch.from_numpy(((A + A.T) / 2).astype(np.float32)).to(cuda)
+    Q = torch.from_numpy(rng.standard_normal((d, p)).astype(np.float32)).to(cuda)
+    Y = de.sym_apply(S, Q)
+    Y2 = torch.full_like(Y, 7.0)
+    de.sym_apply(S, Q, out=Y2, prepared=True, kernel_only=True)
+    torch.cuda.synchronize()
+    assert torch.all(Y2 == 7.0)
+    Y3 = de.sym_apply(S, Q, prepared=True)
+    assert torch.equal(Y, Y3)
