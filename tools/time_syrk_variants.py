@@ -18,7 +18,8 @@ from distributed_eigenspaces_amd import synthetic  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else (1 << 21)
 d = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
 settings = sys.argv[3:] or ["162", "22"]
-KEYS = ("DEIG_SYRK_VARIANT", "DEIG_SYRK_FLUSH_ROWS", "DEIG_SYRK_PRIO", "DEIG_SYRK_PACE")
+KEYS = ("DEIG_SYRK_VARIANT", "DEIG_SYRK_FLUSH_ROWS", "DEIG_SYRK_PRIO", "DEIG_SYRK_PACE",
+        "DEIG_SYRK_SEGS")
 
 
 def apply(setting):
