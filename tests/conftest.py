@@ -20,6 +20,12 @@ def load_golden(name):
     """Golden fixture (inputs + reference outputs) as a dict; X as float64 + float32."""
     z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     out = {k: z[k] for k in z.files}
+    if "Xq" not in out and "seed" in out:  # seeded fixture: regenerate the samples
+        from tests.golden_data import spiked_int_data, xq_digest
+        Xq, _ = spiked_int_data(int(out["n"]), int(out["d"]), int(out["k"]), int(out["seed"]),
+                                grid=float(out["grid"]))
+        assert xq_digest(Xq) == str(out["xq_sha256"]), f"{name}: regenerated samples differ"
+        out["Xq"] = Xq
     if "Xq" in out:
         out["X"] = out["Xq"].astype(np.float64) / float(out["grid"])
     return out

@@ -118,18 +118,8 @@ def eigh_shim(a, eigvals=None, **kw):
 
 
 # ----------------------------------------------------------------------------- data
-def spiked_int_data(n, d, k, seed, theta_hi=8.0, theta_lo=4.0, grid=8):
-    """Spiked-covariance rows X = G + H diag(sqrt(theta)) U^T rounded to 1/grid.
-
-    Values are exactly representable in fp32 (and in int16 after * grid) so the
-    same numbers feed the float64 reference and the fp32 GPU path.
-    """
-    rng = np.random.default_rng(seed)
-    U, _ = np.linalg.qr(rng.standard_normal((d, k)))
-    theta = np.linspace(theta_hi, theta_lo, k)
-    X = rng.standard_normal((n, d)) + (rng.standard_normal((n, k)) * np.sqrt(theta)) @ U.T
-    Xq = np.clip(np.round(X * grid), -32767, 32767).astype(np.int16)
-    return Xq, U
+sys.path.insert(0, os.path.dirname(OUT))  # tests/: golden_data (the input generator)
+from golden_data import spiked_int_data, xq_digest  # noqa: E402
 
 
 def import_reference():
@@ -233,6 +223,9 @@ def main():
         ("spiked_d256_k10_m8", 8 * 320, 256, 10, 8, 13, True, True),
         ("spiked_d256_k16_m4", 4 * 300, 256, 16, 4, 14, False, False),
         ("spiked_d1024_k16_m1", 1200, 1024, 16, 1, 15, False, False),
+        # config-2 width (d = 3072); inputs regenerated from the seed by the tests
+        # (tests/golden_data.py, pinned by xq_sha256): 37 MB of samples not stored
+        ("spiked_d3072_k16_m2_seeded", 2 * 3200, 3072, 16, 2, 16, False, False),
     ]
     for name, n, d, k, m, seed, proto, store_s in cases:
         Xq, U = spiked_int_data(n, d, k, seed, grid=grid)
@@ -240,6 +233,10 @@ def main():
         res = (run_protocol if proto else direct_workers)(distributed, data, k, m)
         out = dict(Xq=Xq, grid=np.float64(grid), k=np.int64(k), m=np.int64(m),
                    U_planted=U.astype(np.float32), **res)
+        if name.endswith("_seeded"):
+            out.pop("Xq")
+            out.update(seed=np.int64(seed), n=np.int64(n), d=np.int64(d),
+                       xq_sha256=np.array(xq_digest(Xq)))
         if not store_s or d > 256:
             out.pop("sigma_tilde")
         if store_s:
