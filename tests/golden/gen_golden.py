@@ -226,8 +226,14 @@ def main():
         # config-2 width (d = 3072); inputs regenerated from the seed by the tests
         # (tests/golden_data.py, pinned by xq_sha256): 37 MB of samples not stored
         ("spiked_d3072_k16_m2_seeded", 2 * 3200, 3072, 16, 2, 16, False, False),
+        # config-3 width and k (d = 8192, k = 64): one 16384-row shard (the top-64
+        # subspace is well separated there: lambda_64 ~ 5 vs the noise edge ~ 2.9)
+        ("spiked_d8192_k64_m1_seeded", 16384, 8192, 64, 1, 17, False, False),
     ]
+    only = set(sys.argv[1:])  # optional: regenerate just the named cases
     for name, n, d, k, m, seed, proto, store_s in cases:
+        if only and name not in only:
+            continue
         Xq, U = spiked_int_data(n, d, k, seed, grid=grid)
         data = Xq.astype(np.float64) / grid  # float64 like distributed.py:171
         res = (run_protocol if proto else direct_workers)(distributed, data, k, m)
@@ -235,6 +241,8 @@ def main():
                    U_planted=U.astype(np.float32), **res)
         if name.endswith("_seeded"):
             out.pop("Xq")
+            if d > 4096:
+                out.pop("U_planted")  # regenerable from the seed; keeps the fixture small
             out.update(seed=np.int64(seed), n=np.int64(n), d=np.int64(d),
                        xq_sha256=np.array(xq_digest(Xq)))
         if not store_s or d > 256:
@@ -246,6 +254,8 @@ def main():
         np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
         print("wrote", name, {k_: getattr(v, "shape", v) for k_, v in out.items()})
 
+    if only:
+        return 0
     # notebook online loop (m=10, T=10, k=2 are hard-coded in the cell; raw 277-279)
     Xq, _ = spiked_int_data(10 * 96 + 37, 64, 2, 21, grid=grid)
     data = Xq.astype(np.float64) / grid

@@ -12,14 +12,14 @@ import pytest
 import torch
 
 from oracle import ref_cpu
-from tests.conftest import golden_names, load_golden
+from tests.conftest import golden_keys, golden_names, load_golden
 
 pytestmark = pytest.mark.gpu
 P_TOL, EV_TOL = 1e-4, 1e-5
 
 
 @pytest.mark.parametrize("name", [n for n in golden_names()
-                                  if "request_ranges" in load_golden(n)])
+                                  if "request_ranges" in golden_keys(n)])
 def test_protocol_end_to_end_golden(name, cuda):
     """SlaveNode/MasterNode over the in-process broker == the reference run."""
     from distributed_eigenspaces_amd import broker as br
