@@ -163,7 +163,7 @@ def run_protocol(distributed, data, rank, batches_number):
                 sigma_tilde=sigma_tilde)
 
 
-def direct_workers(distributed, data, rank, batches_number):
+def direct_workers(distributed, data, rank, batches_number, server=True):
     """Worker math of distributed.py:46-48 for each shard of :99-104 (m < 5 cannot
     run the protocol: the window of 5 at :108 pops an empty list)."""
     step = data.shape[0] // batches_number
@@ -175,6 +175,8 @@ def direct_workers(distributed, data, rank, batches_number):
         V = distributed.Node.top_k_eigenvectors(None, S, rank)
         ranges.append((lo, hi)); Vs.append(V); evs.append(EIGVALS_LOG[-1])
     Vs = np.stack(Vs)
+    if not server:
+        return dict(ranges=np.array(ranges), worker_V=Vs, worker_evals=np.stack(evs))
     d = Vs.shape[1]
     sigma_tilde = np.zeros((d, d))
     for e in Vs:
@@ -229,6 +231,10 @@ def main():
         # config-3 width and k (d = 8192, k = 64): one 16384-row shard (the top-64
         # subspace is well separated there: lambda_64 ~ 5 vs the noise edge ~ 2.9)
         ("spiked_d8192_k64_m1_seeded", 16384, 8192, 64, 1, 17, False, False),
+        # config-5 width and k (d = 16384, k = 128: the subspace the solver runs with
+        # p = k, no guard columns): one 32768-row shard; the worker outputs only,
+        # stored as float32 (16 MB of float64 otherwise; the tests' bars are 1e-4 / 1e-5)
+        ("spiked_d16384_k128_m1_seeded", 32768, 16384, 128, 1, 18, False, False),
     ]
     only = set(sys.argv[1:])  # optional: regenerate just the named cases
     for name, n, d, k, m, seed, proto, store_s in cases:
@@ -236,16 +242,21 @@ def main():
             continue
         Xq, U = spiked_int_data(n, d, k, seed, grid=grid)
         data = Xq.astype(np.float64) / grid  # float64 like distributed.py:171
-        res = (run_protocol if proto else direct_workers)(distributed, data, k, m)
+        if proto:
+            res = run_protocol(distributed, data, k, m)
+        else:
+            res = direct_workers(distributed, data, k, m, server=d <= 8192)
         out = dict(Xq=Xq, grid=np.float64(grid), k=np.int64(k), m=np.int64(m),
                    U_planted=U.astype(np.float32), **res)
         if name.endswith("_seeded"):
             out.pop("Xq")
             if d > 4096:
                 out.pop("U_planted")  # regenerable from the seed; keeps the fixture small
+            if d > 8192:
+                out["worker_V"] = out["worker_V"].astype(np.float32)
             out.update(seed=np.int64(seed), n=np.int64(n), d=np.int64(d),
                        xq_sha256=np.array(xq_digest(Xq)))
-        if not store_s or d > 256:
+        if (not store_s or d > 256) and "sigma_tilde" in out:
             out.pop("sigma_tilde")
         if store_s:
             lo, hi = res["ranges"][0] if not proto else (0, n // m)

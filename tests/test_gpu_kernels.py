@@ -10,7 +10,7 @@ import pytest
 import torch
 
 from oracle import ref_cpu
-from tests.conftest import golden_names, load_golden
+from tests.conftest import golden_keys, golden_names, load_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -160,6 +160,8 @@ def test_worker_path_golden(name, algo, cuda):
 def test_server_golden(name, cuda):
     """Implicit projector-average top-k vs the reference master + NB:306 solve."""
     import distributed_eigenspaces_amd as de
+    if "server_V" not in golden_keys(name):
+        pytest.skip("fixture stores the worker outputs only (d = 16384)")
     g = load_golden(name)
     k, m = int(g["k"]), int(g["m"])
     bases = [torch.from_numpy(v.astype(np.float32)).to(cuda) for v in g["worker_V"]]
@@ -175,9 +177,9 @@ def test_topk_matches_oracle_on_sigma_hat0(cuda):
     """Eigensolver alone on the reference's own float64 Sigma_hat (rounded to fp32)."""
     import distributed_eigenspaces_amd as de
     for name in golden_names():
-        g = load_golden(name)
-        if "sigma_hat0" not in g:
+        if "sigma_hat0" not in golden_keys(name):
             continue
+        g = load_golden(name)
         k = int(g["k"])
         S32 = g["sigma_hat0"].astype(np.float32)
         r = de.topk_eigh(torch.from_numpy(S32).to(cuda), k)
