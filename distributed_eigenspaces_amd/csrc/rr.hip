@@ -141,6 +141,7 @@ __global__ __launch_bounds__(NT) void rr_small_kernel(const float* __restrict__ 
     info[0] = 0;
     info[1] = 0;
     info[2] = 0;
+    info[3] = 0;  // 1 once the Jacobi iteration has converged (not stopped by the cap)
   }
   __syncthreads();
   for (int idx = tid; idx < pp; idx += NT) {
@@ -295,7 +296,10 @@ __global__ __launch_bounds__(NT) void rr_small_kernel(const float* __restrict__ 
         }
       }
       need = __syncthreads_or(need);
-      if (!need) break;
+      if (!need) {
+        if (tid == 0) info[3] = 1;
+        break;
+      }
     }
     for (int st = 0; st < p - 1; ++st) {
       const int ci = 1 + (st & 1);
@@ -374,7 +378,10 @@ __global__ __launch_bounds__(NT) void rr_small_kernel(const float* __restrict__ 
       info[2] += swrot;
     }
     __syncthreads();
-    if (swrot == 0) break;
+    if (swrot == 0) {
+      if (tid == 0) info[3] = 1;
+      break;
+    }
   }
 
   stamp(7);
