@@ -289,12 +289,17 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
   // ~4e-6 relative noise into the basis each sweep, harmless while the Ritz
   // vectors are far from converged, but a floor under the residual, so the
   // closing sweeps use the exact (3-piece) Q.
-  // (r02s A/B, profiles/r02s_jacobi_cap_ab.log: 2 sweeps while the residual is
-  // above 1e-4 - c1 +9 %, c1g +26 % over 3 above 1e-2; 1 sweep fails the bars)
-  static const int jcap_sweeps =
-      getenv("DEIG_JACOBI_EARLY") ? atoi(getenv("DEIG_JACOBI_EARLY")) : 2;
-  static const float jcap_above =
-      getenv("DEIG_JACOBI_EARLY_ABOVE") ? (float)atof(getenv("DEIG_JACOBI_EARLY_ABOVE")) : 1e-4f;
+  // Worker solves (explicit S): 2 sweeps while the residual is above 1e-4 (r02s A/B,
+  // profiles/r02s_jacobi_cap_ab.log: c1 +8 %, c1g +14 % over 3 above 1e-2, c3 the
+  // same time in 16 sweeps instead of 12; 1 sweep fails the bars).  The server's
+  // implicit projector average (eigenvalues clustered near 1) keeps 3 above 1e-2:
+  // there the tighter cap cost config 4's aggregation 2.05 -> 2.65 ms.
+  static const int jcap_env =
+      getenv("DEIG_JACOBI_EARLY") ? atoi(getenv("DEIG_JACOBI_EARLY")) : -1;
+  static const float jcap_above_env =
+      getenv("DEIG_JACOBI_EARLY_ABOVE") ? (float)atof(getenv("DEIG_JACOBI_EARLY_ABOVE")) : -1.f;
+  const int jcap_sweeps = jcap_env >= 0 ? jcap_env : (op.implicit ? 3 : 2);
+  const float jcap_above = jcap_above_env >= 0.f ? jcap_above_env : (op.implicit ? 1e-2f : 1e-4f);
   // Early sweeps (residual above fast_until) take S as its two leading bf16 pieces
   // too: three products, no split in the sweep, ~2^-16 relative - 100x below the
   // residual there (sweep.hip sweep_products SP = 2).  DEIG_SWEEP_FAST_UNTIL=0: off.
@@ -384,7 +389,11 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
       // residual bounds the error, but the eigenvalues / vectors returned are those
       // of an unconverged small solve, so no exit is taken on them - the next RR
       // (the residual is then below jcap_above) runs the Jacobi to convergence.
-      const bool exact_rr = jconv_h != 0;
+      // Needed where the residual is relative to a dominant theta_0 (worker S:
+      // r02s, a 2-sweep cap at every residual missed a CIFAR-gray eigenvalue by
+      // 1.0046e-5); the server's projector average (eigenvalues in [0, 1], top k
+      // near 1) exits as before - guarding it cost c1's server 5 -> 7 sweeps.
+      const bool exact_rr = jconv_h != 0 || op.implicit;
       ++nrr;
       if (debug) {
         int inf[9] = {0};
