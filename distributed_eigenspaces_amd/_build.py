@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdeig.so")
 SOURCES = ["capi.hip", "syrk.hip", "syrk_split.hip", "syrk_u8.hip", "skinny.hip", "rr.hip", "oja.hip",
-           "project.hip", "sweep.hip"]
+           "project.hip", "sweep.hip", "shift.hip"]
 # Per-source extra flags.  sweep.hip: keep the split's scalar f32 subtractions
 # unpacked (v_pk_add_f32 beside MFMAs costs issue cycles, MI355X_MICROARCH.md).
 EXTRA_FLAGS = {"sweep.hip": ["-fno-slp-vectorize"], "syrk_split.hip": ["-fno-slp-vectorize"]}
@@ -37,11 +37,15 @@ def _stale() -> bool:
     return any(os.path.getmtime(p) > t for p in deps)
 
 
-def build_library(force: bool = False, verbose: bool = True) -> str:
-    if not force and not _stale():
+def build_library(force: bool = False, verbose: bool = True, defines=(), out: str | None = None) -> str:
+    """Build libdeig.so (or, with ``defines`` such as ``-DDEIG_AB_SYRK_VARIANT=22``, an
+    A/B variant into ``out`` - measurement tooling only; the shipped library reads
+    no environment and has no knobs)."""
+    lib = out or LIB
+    if not force and not defines and lib == LIB and not _stale():
         return LIB
     objs = []
-    tmpdir = os.path.join(HERE, "build")
+    tmpdir = os.path.join(HERE, "build" if not defines else "build_ab")
     os.makedirs(tmpdir, exist_ok=True)
     hipcc = _hipcc()
     procs = []
@@ -49,7 +53,8 @@ def build_library(force: bool = False, verbose: bool = True) -> str:
         obj = os.path.join(tmpdir, src.replace(".hip", ".o"))
         objs.append(obj)
         cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-               "-Wno-unused-function", "-Wno-inline-asm"] + EXTRA_FLAGS.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
+               "-Wno-unused-function", "-Wno-inline-asm"] + list(defines) + EXTRA_FLAGS.get(src, []) + \
+            ["-c", os.path.join(CSRC, src), "-o", obj]
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
     for cmd, p in procs:
         out, _ = p.communicate()
@@ -57,15 +62,15 @@ def build_library(force: bool = False, verbose: bool = True) -> str:
             raise RuntimeError("hipcc failed:\n" + " ".join(cmd) + "\n" + out.decode())
         if verbose and out.strip():
             sys.stderr.write(out.decode())
-    tmp_lib = LIB + ".tmp"
+    tmp_lib = lib + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp_lib] + objs
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     if r.returncode != 0:
         raise RuntimeError("link failed:\n" + r.stdout.decode())
-    os.replace(tmp_lib, LIB)
+    os.replace(tmp_lib, lib)
     if verbose:
-        sys.stderr.write(f"built {LIB}\n")
-    return LIB
+        sys.stderr.write(f"built {lib}\n")
+    return lib
 
 
 if __name__ == "__main__":

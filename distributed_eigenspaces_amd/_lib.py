@@ -12,7 +12,9 @@ import re
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdeig.so")
+# DEIG_LIB_PATH: an A/B variant built by tools/ (_build.build_library(defines=...));
+# the product default is the in-tree libdeig.so.
+LIB_PATH = os.environ.get("DEIG_LIB_PATH") or os.path.join(HERE, "libdeig.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "deig.h")
 
 DEIG_OK = 0
@@ -35,6 +37,27 @@ SWEEP_ALGOS = {"auto": DEIG_SWEEP_AUTO, "bf16x6": DEIG_SWEEP_BF16X6, "fp32": DEI
 DEIG_U8_RAW = 0
 DEIG_U8_GRAY3 = 1
 U8_MODES = {"raw": DEIG_U8_RAW, "gray": DEIG_U8_GRAY3}
+DEIG_F32 = 0
+DEIG_F64 = 1
+
+
+class SolverOpts(ctypes.Structure):
+    """``deig_solver_opts`` (include/deig.h); build with :func:`solver_opts`."""
+
+    _fields_ = [
+        ("size", ctypes.c_int),
+        ("sweep_algo", ctypes.c_int),
+        ("rr_every", ctypes.c_int),
+        ("chebyshev", ctypes.c_int),
+        ("cheb_above", ctypes.c_float),
+        ("deflate", ctypes.c_int),
+        ("deflate_early", ctypes.c_int),
+        ("jacobi_early_sweeps", ctypes.c_int),
+        ("jacobi_early_above", ctypes.c_float),
+        ("fast_until", ctypes.c_float),
+        ("round_until", ctypes.c_float),
+        ("debug", ctypes.c_int),
+    ]
 
 _c_i64 = ctypes.c_int64
 _c_sz = ctypes.c_size_t
@@ -59,6 +82,25 @@ SIGNATURES = {
                                          _fp, _c_i64, _fp, ctypes.POINTER(ctypes.c_int),
                                          ctypes.POINTER(ctypes.c_float), _vp, _c_sz, _vp]),
     "deig_topk_workspace": (_c_sz, [_c_i64, ctypes.c_int, ctypes.c_int]),
+    "deig_solver_opts_init": (None, [ctypes.POINTER(SolverOpts)]),
+    "deig_topk_sym_ex": (ctypes.c_int, [_fp, ctypes.c_int, _c_i64, _c_i64, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_float, _fp, ctypes.c_int, _c_i64,
+                                        _fp, _c_i64, _fp, ctypes.POINTER(ctypes.c_int),
+                                        ctypes.POINTER(ctypes.c_float), ctypes.POINTER(SolverOpts),
+                                        _vp, _c_sz, _vp]),
+    "deig_topk_workspace_ex": (_c_sz, [_c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(SolverOpts)]),
+    "deig_projavg_topk_ex": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, ctypes.c_float,
+                                            ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_float, _fp, ctypes.c_int, _c_i64, _fp,
+                                            _c_i64, _fp, ctypes.POINTER(ctypes.c_int),
+                                            ctypes.POINTER(ctypes.c_float),
+                                            ctypes.POINTER(SolverOpts), _vp, _c_sz, _vp]),
+    "deig_projavg_workspace_ex": (_c_sz, [_c_i64, _c_i64, ctypes.c_int, ctypes.c_int,
+                                          ctypes.POINTER(SolverOpts)]),
+    "deig_syrk_shift": (ctypes.c_int, [_fp, ctypes.c_int, _c_i64, _c_i64, _c_i64, ctypes.c_double,
+                                       _fp, _c_i64, _fp, _c_i64, _vp, _c_sz, _vp]),
+    "deig_syrk_shift_workspace": (_c_sz, [_c_i64, _c_i64, ctypes.c_int]),
     "deig_projavg_topk_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, ctypes.c_float,
                                              ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_float, _fp, ctypes.c_int, _c_i64, _fp,
@@ -122,6 +164,19 @@ def lib() -> ctypes.CDLL:
                 fn.argtypes = args
             _lib = L
     return _lib
+
+
+def solver_opts(**fields) -> SolverOpts:
+    """Solver options: the library defaults (deig_solver_opts_init) with ``fields``
+    overridden; DEIG_DEBUG=1 in the environment turns on the per-RR trace."""
+    o = SolverOpts()
+    lib().deig_solver_opts_init(ctypes.byref(o))
+    if os.environ.get("DEIG_DEBUG", "") == "1":
+        o.debug = 1
+    for name, value in fields.items():
+        if value is not None:
+            setattr(o, name, value)
+    return o
 
 
 def last_error() -> str:

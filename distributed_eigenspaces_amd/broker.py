@@ -27,6 +27,7 @@ unacknowledged ones of a connection that closes are requeued at the front.
 from __future__ import annotations
 
 import json
+import queue
 import socket
 import struct
 import threading
@@ -246,7 +247,10 @@ def _recv(sock):
 
 
 class _Client:
-    """Server-side state of one client connection."""
+    """Server-side state of one client connection.  Deliveries go through an outbox
+    drained by the client's own sender thread, so a consumer that stops reading (a
+    master busy in its callback, a stalled process) blocks only its own socket
+    writes - never the broker lock that every other connection needs."""
 
     def __init__(self, sock):
         self.sock = sock
@@ -254,6 +258,26 @@ class _Client:
         self.queues = set()   # queues this connection consumes
         self.unacked = {}     # tag -> (queue, body)
         self.alive = True
+        self.outbox = queue.SimpleQueue()
+        self.sender = threading.Thread(target=self._send_loop, daemon=True)
+        self.sender.start()
+
+    def _send_loop(self):
+        while True:
+            obj = self.outbox.get()
+            if obj is None:
+                return
+            try:
+                _send(self.sock, obj, self.lock)
+            except OSError:
+                # dead peer: closing the socket ends the reader, which requeues the
+                # unacked deliveries (SocketBroker._serve_client)
+                self.alive = False
+                try:
+                    self.sock.shutdown(socket.SHUT_RDWR)
+                except OSError:
+                    pass
+                return
 
 
 class SocketBroker:
@@ -329,11 +353,7 @@ class SocketBroker:
             self._tag += 1
             c.unacked[self._tag] = (q, body)
             self.delivered.append((q, body))
-            try:
-                _send(c.sock, {"op": "deliver", "queue": q, "tag": self._tag, "body": body}, c.lock)
-            except OSError:
-                c.alive = False
-                dq.appendleft(c.unacked.pop(self._tag)[1])
+            c.outbox.put({"op": "deliver", "queue": q, "tag": self._tag, "body": body})
 
     def _serve_client(self, c: _Client):
         try:
@@ -364,6 +384,7 @@ class SocketBroker:
         except OSError:
             pass
         finally:
+            c.outbox.put(None)  # stop the sender
             with self.lock:
                 c.alive = False
                 for q in list(c.queues):

@@ -1,13 +1,15 @@
 // extern "C" boundary of libdeig.so (declared in include/deig.h) and the host
 // drivers of the two eigensolvers.  No device allocation happens here: all
-// device memory is caller-provided (PyTorch tensors on the Python side).
+// device memory is caller-provided (PyTorch tensors on the Python side).  No
+// process-global mutable state: the error string is thread-local, the per-device
+// CU counts are atomics, solver behaviour comes from the caller's options.
 #include <stdarg.h>
 #include <stdio.h>
-#include <stdlib.h>
 #include <string.h>
 #include <math.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "deig_internal.hpp"
 
@@ -31,71 +33,115 @@ int fail(int code, const char* fmt, ...) {
 }
 
 int num_cus() {
-  static int cache[64] = {0};
+  static std::atomic<int> cache[64];  // zero-initialised (static storage)
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
     (void)hipGetLastError();
     return 256;  // MI355X; only reached by workspace queries without a device
   }
-  if (!cache[dev]) {
-    int v = 0;
+  int v = cache[dev].load(std::memory_order_relaxed);
+  if (!v) {
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         v <= 0) {
       (void)hipGetLastError();
       v = 256;
     }
-    cache[dev] = v;
+    cache[dev].store(v, std::memory_order_relaxed);  // same value from every thread
   }
-  return cache[dev];
+  return v;
 }
 
 namespace {
 
 constexpr int kMaxP = 128;
-// Stagnation handling of the solver (see solve()): a stalled residual counts as
+// Block locking (k > kMaxP): each block targets kMaxP - kGuard pairs with kGuard
+// guard columns, then locks them and deflates them out of the operator.
+constexpr int kGuard = 16;
+// Stagnation handling of the solver (see iterate()): a stalled residual counts as
 // converged when <= max(kStallAcceptTol * tol, kStallAcceptAbs) - the fp32 floor
 // of ||S v - lambda v|| / |lambda_max| is a few 1e-7 up to d = 16384 - and the
 // solver gives up after kStallGiveUp Rayleigh-Ritz steps without a 10% gain.
 constexpr float kStallAcceptTol = 4.0f;
 constexpr float kStallAcceptAbs = 2e-6f;
 constexpr int kStallGiveUp = 12;
-// Deflation stage of the explicit-matrix solver (see solve()): eigenpairs with
-// theta_j >= kDeflateRatio * theta_{k-1} (at most kMaxDeflate of them) are
-// deflated out of the sweep image and the rest iterated again.
+// Deflation of dominant pairs (see solve()): eigenpairs with theta_j >=
+// kDeflateRatio * theta_{k-1} (at most kMaxDeflate of them) are locked, deflated
+// out of the operator and the rest iterated again.
 constexpr float kDeflateRatio = 64.f;
 constexpr int kMaxDeflate = 8;
+// Indefinite input: a block whose Ritz values include theta_min < -max(kNegRel *
+// scale, kNegTarget * theta_target) restarts the solve on S + sigma I,
+// sigma = kShiftGrow * |theta_min| (at most kMaxShifts restarts).
+constexpr float kNegRel = 1e-5f;
+constexpr float kNegTarget = 0.1f;
+constexpr double kShiftGrow = 1.1;
+constexpr int kMaxShifts = 2;
+constexpr double kChebGmax = 1e4;
+constexpr int kChebMaxDeg = 16;
+
+struct Opts {
+  int sweep_algo = DEIG_SWEEP_BF16X6;
+  int rr_every = 0;
+  bool cheb = true;
+  float cheb_above = 1e-2f;
+  bool deflate = true;
+  bool deflate_early = true;
+  int jcap_sweeps = -1;
+  float jcap_above = -1.f;
+  float fast_until = 1e-3f;
+  float round_until = 1e-4f;
+  bool debug = false;
+};
+
+Opts make_opts(const deig_solver_opts* o) {
+  Opts r;
+  if (!o) return r;
+  r.sweep_algo = o->sweep_algo == DEIG_SWEEP_FP32 ? DEIG_SWEEP_FP32 : DEIG_SWEEP_BF16X6;
+  r.rr_every = o->rr_every;
+  r.cheb = o->chebyshev != 0;
+  r.cheb_above = o->cheb_above;
+  r.deflate = o->deflate != 0;
+  r.deflate_early = o->deflate_early != 0;
+  r.jcap_sweeps = o->jacobi_early_sweeps;
+  r.jcap_above = o->jacobi_early_above;
+  r.fast_until = o->fast_until;
+  r.round_until = o->round_until;
+  r.debug = o->debug != 0;
+  return r;
+}
 
 struct Operator {
   bool implicit;
-  const float* S;
+  const void* S;  // explicit: d x d row-major (lds), element type stype
+  int stype;
   int64_t lds;
-  const float* Wt;
+  const float* Wt;  // implicit: scale * Wt^T Wt
   int64_t mk, ldw;
   float scale;
+  // applied on top of the base operator (image: folded in by sweep_prepare;
+  // plain products: applied after each product): + shift I - Vd diag(lamd) Vd^T
+  double shift;
+  const float* Vd;
+  int64_t ldvd;
+  const float* lamd;
+  int r;
 };
 
 struct SolverWs {
   RRBuffers rr;
   float* Zt;
-  float* T;  // d x p: X_{j-1} of the Chebyshev recurrence
+  float* T;     // d x p: X_{j-1} of the Chebyshev recurrence
+  float* Tdef;  // k x p: Vd^T Q of the plain-product deflation
   float* slab;
   size_t slab_bytes;
-  void* sweep_ws;  // bf16x6 sweep (explicit S only)
+  void* sweep_ws;  // bf16x6 sweep image (explicit S only)
   size_t sweep_bytes;
 };
 
-// Sweep algorithm of the explicit-matrix solver: DEIG_SWEEP_ALGO=fp32 selects the
-// f32 MFMA skinny kernel, anything else the bf16x6 sweep (sweep.hip).
-int sweep_algo_default() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DEIG_SWEEP_ALGO");
-    v = (e && strcmp(e, "fp32") == 0) ? DEIG_SWEEP_FP32 : DEIG_SWEEP_BF16X6;
-  }
-  return v;
-}
-
-SolverWs carve_solver(void* ws, size_t cap, int64_t d, int k, int p, int64_t mk, size_t* total) {
+// p: the widest block subspace, kb: the most pairs one block targets (<= p), k:
+// all pairs (locked ones are deflated by plain products when there is no image).
+SolverWs carve_solver(void* ws, size_t cap, int64_t d, int kb, int k, int p, int64_t mk,
+                      bool image, size_t* total) {
   Carve c(ws, cap);
   SolverWs w;
   w.rr.Z = c.take<float>((size_t)d * 2 * p);
@@ -106,26 +152,32 @@ SolverWs carve_solver(void* ws, size_t cap, int64_t d, int k, int p, int64_t mk,
   w.rr.lam = c.take<float>((size_t)p);
   w.rr.cs = c.take<float>((size_t)p);
   w.rr.qs = c.take<float>((size_t)p);
-  w.rr.resid_part = c.take<float>((size_t)rr_update_blocks(d) * k);
-  w.rr.resid = c.take<float>((size_t)k + 1);
+  w.rr.resid_part = c.take<float>((size_t)rr_update_blocks(d) * kb);
+  w.rr.resid = c.take<float>((size_t)kb + 1);
   w.rr.info = c.take<int>(16);
   w.Zt = mk > 0 ? c.take<float>((size_t)mk * p) : nullptr;
   w.T = c.take<float>((size_t)d * p);
+  w.Tdef = image ? nullptr : c.take<float>((size_t)k * p);
   size_t sb = skinny_workspace_bytes(2 * p, 2 * p, d);  // Gram
-  if (mk > 0) {
-    const size_t a = skinny_workspace_bytes(mk, p, d);  // Wt Q
-    const size_t b = skinny_workspace_bytes(d, p, mk);  // Wt^T Zt
-    if (a > sb) sb = a;
+  auto need = [&](int64_t M, int64_t N, int64_t K) {
+    const size_t b = skinny_workspace_bytes(M, N, K);
     if (b > sb) sb = b;
-  } else {
-    const size_t a = skinny_workspace_bytes(d, p, d);  // S Q
-    if (a > sb) sb = a;
+  };
+  if (mk > 0) {
+    need(mk, p, d);  // Wt Q
+    need(d, p, mk);  // Wt^T Zt
+  } else if (!image) {
+    need(d, p, d);  // S Q
+  }
+  if (!image) {  // plain-product deflation: Vd^T Q and Vd T
+    need(k, p, d);
+    need(d, p, k);
   }
   w.slab = c.take<float>(sb / sizeof(float) + 4);
   w.slab_bytes = sb;
   w.sweep_ws = nullptr;
   w.sweep_bytes = 0;
-  if (mk == 0 && sweep_algo_default() == DEIG_SWEEP_BF16X6) {
+  if (image) {
     w.sweep_bytes = sweep_workspace_bytes(d, p);
     w.sweep_ws = c.take<char>(w.sweep_bytes);
   }
@@ -133,20 +185,64 @@ SolverWs carve_solver(void* ws, size_t cap, int64_t d, int k, int p, int64_t mk,
   return w;
 }
 
+// Y[r][:] += s Q[r][:] (row strides ldy, ldq; p columns) - the shift on plain products.
+__global__ __launch_bounds__(256) void axpy_rows_kernel(float* __restrict__ Y, int64_t ldy,
+                                                        const float* __restrict__ Q, int64_t ldq,
+                                                        int64_t d, int p, float s) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= d * p) return;
+  const int64_t r = idx / p;
+  const int j = (int)(idx - r * p);
+  Y[r * ldy + j] = fmaf(s, Q[r * ldq + j], Y[r * ldy + j]);
+}
+
+// T[q][:] *= -lam[q]  (r x p, row stride p).
+__global__ __launch_bounds__(256) void neg_scale_rows_kernel(float* __restrict__ T, int r, int p,
+                                                             const float* __restrict__ lam) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)r * p) return;
+  T[idx] *= -lam[idx / p];
+}
+
 // Y = A Q without a sweep image: the fp32 skinny product (explicit S) or the
-// implicit projector average Wt^T (Wt Q) (the server).
+// implicit projector average Wt^T (Wt Q) (the server), then the shift and the
+// deflation of the locked pairs as products with Vd.
 int apply_op_plain(const Operator& op, const SolverWs& w, int64_t d, int p, hipStream_t st) {
   float* Q = w.rr.Z;
   float* Y = w.rr.Z + p;
   const int64_t ld = 2 * p;
-  if (!op.implicit)
-    return skinny_launch(true, op.S, op.lds, Q, ld, Y, ld, d, p, d, 1.f, 0.f, w.slab,
-                         w.slab_bytes, st);
-  int rc = skinny_launch(false, op.Wt, op.ldw, Q, ld, w.Zt, p, op.mk, p, d, 1.f, 0.f, w.slab,
-                         w.slab_bytes, st);
-  if (rc) return rc;
-  return skinny_launch(true, op.Wt, op.ldw, w.Zt, p, Y, ld, d, p, op.mk, op.scale, 0.f, w.slab,
+  int rc;
+  if (!op.implicit) {
+    rc = skinny_launch(true, static_cast<const float*>(op.S), op.lds, Q, ld, Y, ld, d, p, d, 1.f,
+                       0.f, w.slab, w.slab_bytes, st);
+  } else {
+    rc = skinny_launch(false, op.Wt, op.ldw, Q, ld, w.Zt, p, op.mk, p, d, 1.f, 0.f, w.slab,
                        w.slab_bytes, st);
+    if (rc) return rc;
+    rc = skinny_launch(true, op.Wt, op.ldw, w.Zt, p, Y, ld, d, p, op.mk, op.scale, 0.f, w.slab,
+                       w.slab_bytes, st);
+  }
+  if (rc) return rc;
+  if (op.shift != 0.0) {
+    hipLaunchKernelGGL(axpy_rows_kernel, dim3((unsigned)cdiv(d * p, 256)), dim3(256), 0, st, Y, ld,
+                       Q, ld, d, p, (float)op.shift);
+    DEIG_HIP_CHECK(hipGetLastError());
+  }
+  if (op.r > 0) {
+    DEIG_REQUIRE(op.ldvd % 4 == 0, "solver: deflation needs ldv %% 4 == 0 (ldv=%lld)",
+                 (long long)op.ldvd);
+    // Tdef = Vd^T Q (Vd column-major = r x d row-major), scaled by -lam, Y += Vd Tdef
+    if ((rc = skinny_launch(false, op.Vd, op.ldvd, Q, ld, w.Tdef, p, op.r, p, d, 1.f, 0.f, w.slab,
+                            w.slab_bytes, st)))
+      return rc;
+    hipLaunchKernelGGL(neg_scale_rows_kernel, dim3((unsigned)cdiv((int64_t)op.r * p, 256)),
+                       dim3(256), 0, st, w.Tdef, op.r, p, op.lamd);
+    DEIG_HIP_CHECK(hipGetLastError());
+    if ((rc = skinny_launch(true, op.Vd, op.ldvd, w.Tdef, p, Y, ld, d, p, op.r, 1.f, 1.f, w.slab,
+                            w.slab_bytes, st)))
+      return rc;
+  }
+  return DEIG_OK;
 }
 
 // Y = A Q.  step (optional): the basis step that follows (power / Chebyshev).  On
@@ -159,49 +255,36 @@ int apply_op(const Operator& op, const SolverWs& w, int64_t d, int p, hipStream_
   float* Q = w.rr.Z;
   float* Y = w.rr.Z + p;
   const int64_t ld = 2 * p;
-  if (!op.implicit && w.sweep_ws)
-    return sweep_apply(op.S, d, op.lds, Q, p, ld, Y, ld, 1.f, w.sweep_ws, w.sweep_bytes, st,
-                       smode, step, q_ready);
+  if (w.sweep_ws)
+    return sweep_apply(Q, d, p, ld, Y, ld, 1.f, w.sweep_ws, w.sweep_bytes, st, smode, step, q_ready);
   int rc = apply_op_plain(op, w, d, p, st);
   if (rc || !step) return rc;
   if (step->kind == 1) return rr_power_launch(w.rr, d, p, step->tau, st);
   return cheb_step_launch(w.rr, w.T, d, p, step->thr, step->a, step->cc, step->gamma, st);
 }
 
-// Whether apply_op fuses steps and Q images (the q_ready protocol applies).
-bool fused_steps(const Operator& op, const SolverWs& w) { return !op.implicit && w.sweep_ws; }
-
-
 // Chebyshev filter plan for the sweeps between two Rayleigh-Ritz steps (host side,
 // from the last RR's Ritz values theta_0 >= ... >= theta_{p-1} and residual).
-// The operator is assumed PSD (covariances, projector averages): the damped
-// interval is [0, c] with c = theta_{p-1} (the block's smallest Ritz value) when
-// the basis has guard columns, else min(theta_{p-1}, theta_{k-1} / 2).  Scaled
-// recurrence at gamma = theta_0 (Zhou & Saad): X_1 = (s1/e)(A - cc) X_0,
-// X_{j+1} = (2 s_{j+1}/e)(A - cc) X_j - s_j s_{j+1} X_{j-1}, s_{j+1} = 1/(2/s1 - s_j).
-// Degree m: at most kChebMaxDeg, at most what the residual still needs at column
-// k's damping rate, and small enough that a column's contamination by theta_0's
-// direction grows at most gmax = clamp(1/resid, 10, kChebGmax) times (the fp32
-// Gram of the filtered block must still resolve every column); columns whose
-// growth would exceed gmax stay out of the filter (threshold thr on theta_j).
-// Only used once resid <= kChebAbove: before that the Ritz values are too rough
-// to place the interval, and plain power steps run.
-constexpr float kChebAbove = 1e-2f;
-float cheb_above() {  // DEIG_CHEB_ABOVE overrides (A/B)
-  static const float v = getenv("DEIG_CHEB_ABOVE") ? (float)atof(getenv("DEIG_CHEB_ABOVE")) : kChebAbove;
-  return v;
-}
-constexpr double kChebGmax = 1e4;
-constexpr int kChebMaxDeg = 16;
-
+// The operator is PSD here (covariances, projector averages, or an indefinite S
+// shifted by the solver): the damped interval is [0, c] with c = theta_{p-1} (the
+// block's smallest Ritz value) when the basis has guard columns, else
+// min(theta_{p-1}, theta_{k-1} / 2).  Scaled recurrence at gamma = theta_0 (Zhou &
+// Saad): X_1 = (s1/e)(A - cc) X_0, X_{j+1} = (2 s_{j+1}/e)(A - cc) X_j - s_j s_{j+1}
+// X_{j-1}, s_{j+1} = 1/(2/s1 - s_j).  Degree m: at most kChebMaxDeg, at most what
+// the residual still needs at column k's damping rate, and small enough that a
+// column's contamination by theta_0's direction grows at most gmax = clamp(1/resid,
+// 10, kChebGmax) times (the fp32 Gram of the filtered block must still resolve
+// every column); columns whose growth would exceed gmax stay out of the filter
+// (threshold thr on theta_j).  Only used once resid <= cheb_above: before that the
+// Ritz values are too rough to place the interval, and plain power steps run.
 struct ChebPlan {
   int m = 0;
   double cc = 0, e = 1, s1 = 0;
   float thr = 0;
 };
 
-bool cheb_plan(const float* lam, int k, int p, float resid, float tol, ChebPlan* pl) {
-  if (!(resid <= cheb_above()) || !(resid > 0)) return false;
+bool cheb_plan(const float* lam, int k, int p, float resid, float tol, float above, ChebPlan* pl) {
+  if (!(resid <= above) || !(resid > 0)) return false;
   const double gmax = fmin(kChebGmax, fmax(10.0, 1.0 / (double)resid));
   const double a = 0.0;
   double c = lam[p - 1];
@@ -224,118 +307,82 @@ bool cheb_plan(const float* lam, int k, int p, float resid, float tol, ChebPlan*
   return true;
 }
 
-int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol, const float* Q0,
-          int k0, int64_t ldq0, float* V, int64_t ldv, float* evals, int* sweeps_out,
-          float* resid_out, void* ws, size_t ws_bytes, hipStream_t st) {
-  DEIG_REQUIRE(d >= 16 && d % 4 == 0, "solver: d=%lld must be >= 16 and a multiple of 4",
-               (long long)d);
-  DEIG_REQUIRE(k >= 1 && k <= d, "solver: need 1 <= k <= d (k=%d, d=%lld)", k, (long long)d);
-  if (p <= 0) p = deig_default_subspace(d, k);
-  DEIG_REQUIRE(p % 16 == 0 && p >= k && p <= kMaxP && p <= d,
-               "solver: subspace p=%d must be a multiple of 16 with k <= p <= min(128, d)", p);
-  DEIG_REQUIRE(max_sweeps >= 1, "solver: max_sweeps must be >= 1");
-  DEIG_REQUIRE(V && evals && ldv >= d, "solver: bad V / evals / ldv");
-  DEIG_REQUIRE(k0 >= 0 && k0 <= p && (k0 == 0 || (Q0 && ldq0 >= d)), "solver: bad warm start");
-  size_t total = 0;
-  SolverWs w = carve_solver(ws, ws_bytes, d, k, p, op.implicit ? op.mk : 0, &total);
-  if (!ws || total > ws_bytes)
-    return fail(DEIG_EWORKSPACE, "solver: workspace %zu bytes < required %zu", ws_bytes, total);
-
-  static const bool debug = getenv("DEIG_DEBUG") && getenv("DEIG_DEBUG")[0] == '1';
-  // Cycles: [filter / power sweeps] + one sweep with a Rayleigh-Ritz step (Gram +
-  // small solve + update + residual check).  Between two RRs either a Chebyshev
-  // filter of planned degree runs (cheb_plan; DEIG_CHEB=0 disables it) or, while
-  // the residual is above kChebAbove, rr_every - 1 plain power steps Q <- A Q on
-  // the Ritz vectors of the last RR (same span as subspace iteration; the
-  // generalised RR copes with the non-orthonormal basis).  The single-workgroup
-  // small solve is the latency-bound part of a cycle, so spacing RRs divides its
-  // cost.  Power steps: every 4th sweep is an RR when the basis has >= 16 guard
-  // columns beyond k (measured: d=8192 k=64 p=80 6.2 vs 9.0 ms, d=3072 k=16 p=32
-  // 1.4 vs 1.9 ms); every 2nd without them (d=16384 k=128 p=128: 23 sweeps /
-  // 47 ms vs 41 / 54 ms).
-  static const int rr_every_env = getenv("DEIG_RR_EVERY") ? atoi(getenv("DEIG_RR_EVERY")) : 0;
-  static const bool cheb_on = !(getenv("DEIG_CHEB") && getenv("DEIG_CHEB")[0] == '0');
-  const int rr_every = rr_every_env > 0 ? rr_every_env : (p - k >= 16 ? 4 : 2);
-  const float tau = rr_every > 1 ? powf(0.1f, 1.0f / (float)(rr_every - 1)) : 0.f;
-  int rc = rr_init_launch(w.rr.Z, d, p, Q0, k0, ldq0, 0x5eed5eedull, st);
-  if (rc) return rc;
-  if (!op.implicit && w.sweep_ws &&
-      (rc = sweep_prepare(op.S, d, op.lds, p, w.sweep_ws, w.sweep_bytes, st)))
-    return rc;
+struct Solver {
+  Operator op;
+  Opts o;
+  int64_t d;
+  int max_sweeps;
+  float tol;
+  SolverWs w;
+  hipStream_t st;
   float lam_h[kMaxP];
   float res_h[kMaxP + 1];  // per-column residuals of the last RR (descending Ritz order)
-  int jconv_h = 1;         // the last RR's Jacobi converged (rr.hip info[3])
-  int it = 0;  // sweeps done (both stages)
+  int it = 0;              // sweeps done (all blocks and restarts)
   float last = 3.4e38f;
   bool converged = false;
-  // Stage 1 may end as soon as the dominant pairs that stage 2 deflates are
-  // converged (their own residuals <= tol), instead of waiting for every column:
-  // with theta_0 ~ 10^4 theta_k (uncentered data) the Chebyshev filter of stage 1
-  // is held to degree 1 by the dominant direction's growth bound, so its later
-  // cycles are one sweep per Rayleigh-Ritz step.  DEIG_DEFLATE_EARLY=0: off.
-  static const bool deflate_on = !(getenv("DEIG_DEFLATE") && getenv("DEIG_DEFLATE")[0] == '0');
-  static const bool deflate_early =
-      !(getenv("DEIG_DEFLATE_EARLY") && getenv("DEIG_DEFLATE_EARLY")[0] == '0');
-  const bool can_deflate = deflate_on && !op.implicit && w.sweep_ws && sweep_version() != 1 && k >= 2;
-  auto dominant = [&](int kk) {  // pairs stage 2 would deflate (0: none)
-    if (!(lam_h[kk - 1] > 0.f && lam_h[0] >= kDeflateRatio * lam_h[kk - 1])) return 0;
-    int r = 0;
-    while (r < kk - 1 && r < kMaxDeflate && lam_h[r] >= kDeflateRatio * lam_h[kk - 1]) ++r;
-    return r;
-  };
-  bool early = false;
-  // Sweeps round Q to two bf16 pieces (five products instead of six, sweep.hip
-  // split_q_kernel) while the residual is above round_until: the rounding puts
-  // ~4e-6 relative noise into the basis each sweep, harmless while the Ritz
-  // vectors are far from converged, but a floor under the residual, so the
-  // closing sweeps use the exact (3-piece) Q.
-  // Worker solves (explicit S): 2 sweeps while the residual is above 1e-4 (r02s A/B,
-  // profiles/r02s_jacobi_cap_ab.log: c1 +8 %, c1g +14 % over 3 above 1e-2, c3 the
-  // same time in 16 sweeps instead of 12; 1 sweep fails the bars).  The server's
-  // implicit projector average (eigenvalues clustered near 1) keeps 3 above 1e-2:
-  // there the tighter cap cost config 4's aggregation 2.05 -> 2.65 ms.
-  static const int jcap_env =
-      getenv("DEIG_JACOBI_EARLY") ? atoi(getenv("DEIG_JACOBI_EARLY")) : -1;
-  static const float jcap_above_env =
-      getenv("DEIG_JACOBI_EARLY_ABOVE") ? (float)atof(getenv("DEIG_JACOBI_EARLY_ABOVE")) : -1.f;
-  const int jcap_sweeps = jcap_env >= 0 ? jcap_env : (op.implicit ? 3 : 2);
-  const float jcap_above = jcap_above_env >= 0.f ? jcap_above_env : (op.implicit ? 1e-2f : 1e-4f);
-  // Early sweeps (residual above fast_until) take S as its two leading bf16 pieces
-  // too: three products, no split in the sweep, ~2^-16 relative - 100x below the
-  // residual there (sweep.hip sweep_products SP = 2).  DEIG_SWEEP_FAST_UNTIL=0: off.
-  static const float fast_until =
-      getenv("DEIG_SWEEP_FAST_UNTIL") ? (float)atof(getenv("DEIG_SWEEP_FAST_UNTIL")) : 1e-3f;
-  static const float round_until =
-      getenv("DEIG_SWEEP_ROUND_UNTIL") ? (float)atof(getenv("DEIG_SWEEP_ROUND_UNTIL")) : 1e-4f;
 
-  // One stage of the iteration for the top kc pairs (V / evals columns 0..kc-1).
-  // Returns a status; sets converged / last; advances it.
-  auto iterate = [&](int kc) -> int {
+  // Pairs a block's dominant-pair deflation would lock (0: none).
+  int dominant(int kc) const {
+    if (!(lam_h[kc - 1] > 0.f && lam_h[0] >= kDeflateRatio * lam_h[kc - 1])) return 0;
+    int r = 0;
+    while (r < kc - 1 && r < kMaxDeflate && lam_h[r] >= kDeflateRatio * lam_h[kc - 1]) ++r;
+    return r;
+  }
+
+  // Subspace iteration for the top kc pairs of the current operator on a pb-column
+  // basis (initialised by the caller); the pairs go to Vb / evb (ascending).  early
+  // (optional): stop as soon as the dominant pairs are converged (*early_out).
+  int iterate(int kc, int pb, float* Vb, int64_t ldv, float* evb, bool allow_early,
+              bool* early_out) {
+    // Cycles: [filter / power sweeps] + one sweep with a Rayleigh-Ritz step (Gram +
+    // small solve + update + residual check).  Between two RRs either a Chebyshev
+    // filter of planned degree runs (cheb_plan) or, while the residual is above
+    // cheb_above, rr_every - 1 plain power steps Q <- A Q on the Ritz vectors of the
+    // last RR (same span as subspace iteration; the generalised RR copes with the
+    // non-orthonormal basis).  The single-workgroup small solve is the latency-bound
+    // part of a cycle, so spacing RRs divides its cost.  Power steps: every 4th sweep
+    // is an RR when the basis has >= 16 guard columns beyond k (measured: d=8192
+    // k=64 p=80 6.2 vs 9.0 ms, d=3072 k=16 p=32 1.4 vs 1.9 ms); every 2nd without
+    // them (d=16384 k=128 p=128: 23 sweeps / 47 ms vs 41 / 54 ms).
+    const int rr_every = o.rr_every > 0 ? o.rr_every : (pb - kc >= 16 ? 4 : 2);
+    const float tau = rr_every > 1 ? powf(0.1f, 1.0f / (float)(rr_every - 1)) : 0.f;
+    // Early Rayleigh-Ritz steps run a capped Jacobi: worker solves (explicit S) 2
+    // sweeps while the residual is above 1e-4 (r02s A/B, profiles/r02s_jacobi_cap_ab.log:
+    // c1 +8 %, c1g +14 % over 3 above 1e-2, c3 the same time in 16 sweeps instead of
+    // 12; 1 sweep fails the bars); the server's implicit projector average
+    // (eigenvalues clustered near 1) 3 above 1e-2 (the tighter cap cost config 4's
+    // aggregation 2.05 -> 2.65 ms).
+    const int jcap_sweeps = o.jcap_sweeps >= 0 ? o.jcap_sweeps : (op.implicit ? 3 : 2);
+    const float jcap_above = o.jcap_above >= 0.f ? o.jcap_above : (op.implicit ? 1e-2f : 1e-4f);
+    const bool fuse = w.sweep_ws != nullptr;
     float best = 3.4e38f;
-    int since_best = 0;
-    int nrr = 0;
+    int since_best = 0, nrr = 0, start = it;
     last = 3.4e38f;
     converged = false;
-    while (it < max_sweeps) {
-      const int smode = (fast_until > 0.f && last > fmaxf(fast_until, tol)) ? kSweepFast
-                        : last > fmaxf(round_until, tol)                 ? kSweepRoundQ
-                                                                         : kSweepExact;
+    while (it - start < max_sweeps) {
+      const int budget = max_sweeps - (it - start);
+      // Sweep precision by residual: early sweeps (above fast_until) take S as its
+      // two leading bf16 pieces too - three products, no split in the sweep, ~2^-16
+      // relative, 100x below the residual there (sweep.hip sweep_products SP = 2);
+      // then Q rounded to two pieces (five products) down to round_until; the
+      // closing sweeps exact (the rounding puts ~4e-6 relative noise into the basis
+      // each sweep: a floor under the residual).
+      const int smode = (o.fast_until > 0.f && last > fmaxf(o.fast_until, tol)) ? kSweepFast
+                        : last > fmaxf(o.round_until, tol)                      ? kSweepRoundQ
+                                                                                : kSweepExact;
       ChebPlan plan;
-      const bool cheb = cheb_on && nrr > 0 && cheb_plan(lam_h, kc, p, last, tol, &plan);
-      int ncheb = 0, nstep = 0, rc2;
-      // every sweep of a cycle runs in smode, so a fused step can write the next
-      // sweep's Q image (q_ready from the second sweep of the cycle on)
-      const bool fuse = fused_steps(op, w);
+      const bool cheb = o.cheb && nrr > 0 && cheb_plan(lam_h, kc, pb, last, tol, o.cheb_above, &plan);
+      int ncheb = 0, nstep = 0, rc;
       SweepStep step{};
       step.Q = w.rr.Z;
-      step.ldq = 2 * p;
+      step.ldq = 2 * pb;
       step.T = w.T;
       step.cs = w.rr.cs;
       step.lam = w.rr.lam;
       step.next_mode = smode;
       if (cheb) {
         // degree j: apply A to X_j, then X_{j+1} from X_j, A X_j and X_{j-1}
-        const int m = std::min(plan.m, max_sweeps - it - 1);
+        const int m = std::min(plan.m, budget - 1);
         double s_prev = plan.s1;
         for (int j = 0; j < m; ++j, ++it, ++nstep) {
           double alpha, gamma;
@@ -353,33 +400,32 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
           step.a = (float)alpha;
           step.cc = (float)plan.cc;
           step.gamma = (float)gamma;
-          if ((rc2 = apply_op(op, w, d, p, st, smode, &step, fuse && nstep > 0))) return rc2;
+          if ((rc = apply_op(op, w, d, pb, st, smode, &step, fuse && nstep > 0))) return rc;
         }
         ncheb = m;
       } else if (nrr > 0) {
-        const int npow = std::min(rr_every - 1, max_sweeps - it - 1);
+        const int npow = std::min(rr_every - 1, budget - 1);
         // power steps on the live Ritz columns of the last RR (Q_j <- Y_j / ||Y w_j||)
         step.kind = 1;
         step.tau = tau;
         for (int j = 0; j < npow; ++j, ++it, ++nstep)
-          if ((rc2 = apply_op(op, w, d, p, st, smode, &step, fuse && nstep > 0))) return rc2;
+          if ((rc = apply_op(op, w, d, pb, st, smode, &step, fuse && nstep > 0))) return rc;
       }
-      if ((rc2 = apply_op(op, w, d, p, st, smode, nullptr, fuse && nstep > 0))) return rc2;
+      if ((rc = apply_op(op, w, d, pb, st, smode, nullptr, fuse && nstep > 0))) return rc;
       ++it;
-      if ((rc2 = skinny_launch(true, w.rr.Z, 2 * p, w.rr.Z, 2 * p, w.rr.C, 2 * p, 2 * p, 2 * p,
-                               d, 1.f, 0.f, w.slab, w.slab_bytes, st)))
-        return rc2;
-      // Early Rayleigh-Ritz steps (residual above jcap_above) run a capped number
-      // of Jacobi sweeps: the next basis Y W spans span(Y) for any invertible W, so
-      // subspace progress does not need converged Ritz vectors there; the residual
-      // of approximate pairs only over-states the error (no false convergence).
+      if ((rc = skinny_launch(true, w.rr.Z, 2 * pb, w.rr.Z, 2 * pb, w.rr.C, 2 * pb, 2 * pb, 2 * pb,
+                              d, 1.f, 0.f, w.slab, w.slab_bytes, st)))
+        return rc;
+      // The next basis Y W spans span(Y) for any invertible W, so subspace progress
+      // does not need converged Ritz vectors; the residual of approximate pairs
+      // only over-states the error (no false convergence).
       const int jcap = (jcap_sweeps > 0 && last > jcap_above) ? jcap_sweeps : 30;
-      if ((rc2 = rr_small_launch(w.rr, p, st, jcap))) return rc2;
-      if ((rc2 = rr_update_launch(w.rr, d, p, kc, V, ldv, evals, st))) return rc2;
+      if ((rc = rr_small_launch(w.rr, pb, st, jcap))) return rc;
+      if ((rc = rr_update_launch(w.rr, d, pb, kc, Vb, ldv, evb, st))) return rc;
+      int jconv_h = 1;  // the RR's Jacobi converged (rr.hip info[3])
       DEIG_HIP_CHECK(
           hipMemcpyAsync(res_h, w.rr.resid, sizeof(float) * (kc + 1), hipMemcpyDeviceToHost, st));
-      DEIG_HIP_CHECK(hipMemcpyAsync(lam_h, w.rr.lam, sizeof(float) * p, hipMemcpyDeviceToHost, st));
-      jconv_h = 1;
+      DEIG_HIP_CHECK(hipMemcpyAsync(lam_h, w.rr.lam, sizeof(float) * pb, hipMemcpyDeviceToHost, st));
       if (jcap < 30)
         DEIG_HIP_CHECK(
             hipMemcpyAsync(&jconv_h, w.rr.info + 3, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -395,13 +441,13 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
       // near 1) exits as before - guarding it cost c1's server 5 -> 7 sweeps.
       const bool exact_rr = jconv_h != 0 || op.implicit;
       ++nrr;
-      if (debug) {
+      if (o.debug) {
         int inf[9] = {0};
         DEIG_HIP_CHECK(hipMemcpy(inf, w.rr.info, sizeof(inf), hipMemcpyDeviceToHost));
         fprintf(stderr, "[deig] d=%lld k=%d p=%d sweep %d resid %.3e cheb_deg %d chol_floor %d "
                 "jacobi_sweeps %d rotations %d small-solve us: chol %.1f linv %.1f congr %.1f "
                 "jacobi %.1f tail %.1f\n",
-                (long long)d, kc, p, it, last, ncheb, inf[0], inf[1], inf[2], inf[4] * 0.01,
+                (long long)d, kc, pb, it, last, ncheb, inf[0], inf[1], inf[2], inf[4] * 0.01,
                 (inf[5] - inf[4]) * 0.01, (inf[6] - inf[5]) * 0.01, (inf[7] - inf[6]) * 0.01,
                 (inf[8] - inf[7]) * 0.01);
       }
@@ -412,12 +458,12 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
         converged = true;
         return DEIG_OK;
       }
-      if (kc == k && can_deflate && deflate_early && last == last) {
-        const int r = dominant(k);
+      if (allow_early) {
+        const int r = dominant(kc);
         bool ok = r >= 1;
         for (int j = 0; j < r && ok; ++j) ok = res_h[j] <= tol;
         if (ok) {
-          early = true;
+          *early_out = true;
           return DEIG_OK;
         }
       }
@@ -429,7 +475,7 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
       if (last < 0.9f * best) {
         best = last;
         since_best = 0;
-      } else if (++since_best >= 4 && it >= 8) {
+      } else if (++since_best >= 4 && it - start >= 8) {
         if (last <= fmaxf(kStallAcceptTol * tol, kStallAcceptAbs)) {
           converged = true;
           return DEIG_OK;
@@ -438,48 +484,153 @@ int solve(const Operator& op, int64_t d, int k, int p, int max_sweeps, float tol
       }
     }
     return DEIG_OK;
-  };
+  }
 
-  rc = iterate(k);
-  if (rc) {
-    if (sweeps_out) *sweeps_out = it;
-    if (resid_out) *resid_out = last;
-    return rc;
+  // (Re)build the sweep image of the current operator (explicit S only).
+  int prepare(int pb) {
+    if (!w.sweep_ws) return DEIG_OK;
+    return sweep_prepare(op.S, op.stype, d, op.lds, pb, w.sweep_ws, w.sweep_bytes, st, op.Vd,
+                         op.ldvd, op.lamd, op.r, op.shift);
   }
-  // Stage 2 - deflation of dominant eigenpairs.  With theta_0 >> theta_{k-1} (an
-  // uncentered covariance: the mean direction dwarfs the rest, as for the
-  // reference's CIFAR bytes) every fp32 product S q loses ~log2(theta_0 / theta_k)
-  // bits of the small eigenvalues' directions to cancellation, which caps their
-  // accuracy far above the residual test's reach (relative to theta_0).  The r
-  // leading pairs with theta_j >= kDeflateRatio theta_{k-1} are then accurate
-  // (huge gap), so the sweep image is rebuilt as S - V_D Lam_D V_D^T and the
-  // remaining k - r pairs are iterated again from their current values (warm
-  // start), with the residual now relative to theta_r.  V_D stays in the last r
-  // columns of V (ascending order), which the second stage does not touch.
-  if (can_deflate && (converged || early) && dominant(k) >= 1) {
-    const int r = dominant(k);
-    const int kc = k - r;
-    const float* Vd = V + (int64_t)kc * ldv;
-    if ((rc = sweep_prepare(op.S, d, op.lds, p, w.sweep_ws, w.sweep_bytes, st, Vd, ldv,
-                            evals + kc, r)))
-      return rc;
-    if ((rc = rr_init_launch(w.rr.Z, d, p, V, kc, ldv, 0x5eed5eefull, st))) return rc;
-    rc = iterate(kc);
-    if (!rc) rc = deflate_orth_launch(V, ldv, d, kc, r, st);
-    if (debug)
-      fprintf(stderr, "[deig] deflated %d dominant pair(s)%s: stage 2 resid %.3e after %d sweeps\n",
-              r, early ? " (early)" : "", last, it);
-    if (rc) {
-      if (sweeps_out) *sweeps_out = it;
-      if (resid_out) *resid_out = last;
-      return rc;
+};
+
+int default_subspace(int64_t d, int k) {
+  if (k > kMaxP) return (int)std::min<int64_t>(kMaxP, d / 16 * 16);
+  int64_t p = ((int64_t)k + (k < 16 ? 8 : k / 4) + 15) / 16 * 16;
+  if (p > kMaxP) p = kMaxP;
+  if (p > d) p = d / 16 * 16;
+  if (p < k) p = (k + 15) / 16 * 16;
+  return (int)p;
+}
+
+// Block structure: pairs per full block and the widest block subspace.
+void block_shape(int64_t d, int k, int p_in, int* p_blk, int* kb) {
+  if (k <= kMaxP) {
+    *p_blk = p_in > 0 ? p_in : default_subspace(d, k);
+    *kb = k;
+  } else {
+    *p_blk = p_in > 0 ? p_in : default_subspace(d, k);
+    *kb = *p_blk - kGuard;
+  }
+}
+
+// Top-k eigenpairs (ascending) of the operator.  Blocks of at most kb pairs are
+// solved top-down; each block's converged pairs are LOCKED at the end of V and
+// deflated out of the operator for the blocks below (k > 128 = kMaxP: the Ritz
+// problem of one workgroup holds at most 128 columns).  Within a block, dominant
+// pairs (theta_j >= 64 theta_k, an uncentered covariance's mean direction) are
+// locked first and the rest iterated again on the deflated operator: every fp32
+// product S q otherwise loses log2(theta_0 / theta_k) bits of the small directions
+// to cancellation.  Deflated images are formed in double (sweep_prepare_kernel).
+// A block whose Ritz values show a large negative eigenvalue (S indefinite: the
+// filter and power steps favour large |lambda|) restarts the solve on S + sigma I.
+int solve(const Operator& op0, int64_t d, int k, int p, int max_sweeps, float tol, const float* Q0,
+          int k0, int64_t ldq0, float* V, int64_t ldv, float* evals, int* sweeps_out,
+          float* resid_out, const Opts& o, void* ws, size_t ws_bytes, hipStream_t st) {
+  DEIG_REQUIRE(d >= 16 && d % 4 == 0, "solver: d=%lld must be >= 16 and a multiple of 4",
+               (long long)d);
+  DEIG_REQUIRE(k >= 1 && k <= d, "solver: need 1 <= k <= d (k=%d, d=%lld)", k, (long long)d);
+  int pb0, kb;
+  block_shape(d, k, p, &pb0, &kb);
+  if (k <= kMaxP)
+    DEIG_REQUIRE(pb0 % 16 == 0 && pb0 >= k && pb0 <= kMaxP && pb0 <= d,
+                 "solver: subspace p=%d must be a multiple of 16 with k <= p <= min(128, d)", pb0);
+  else
+    DEIG_REQUIRE(pb0 % 16 == 0 && pb0 >= 2 * kGuard && pb0 <= kMaxP && pb0 <= d,
+                 "solver: k=%d > 128 needs a block subspace p in {32, ..., 128} (p=%d)", k, pb0);
+  DEIG_REQUIRE(max_sweeps >= 1, "solver: max_sweeps must be >= 1");
+  DEIG_REQUIRE(V && evals && ldv >= d, "solver: bad V / evals / ldv");
+  DEIG_REQUIRE(k0 >= 0 && k0 <= pb0 && (k0 == 0 || (Q0 && ldq0 >= d)), "solver: bad warm start");
+  const bool image = !op0.implicit && o.sweep_algo != DEIG_SWEEP_FP32;
+  DEIG_REQUIRE(image || op0.implicit || op0.stype == DEIG_F32,
+               "solver: a float64 S needs the bf16x6 sweep (DEIG_SWEEP_AUTO)");
+  size_t total = 0;
+  Solver sv;
+  sv.w = carve_solver(ws, ws_bytes, d, kb, k, pb0, op0.implicit ? op0.mk : 0, image, &total);
+  if (!ws || total > ws_bytes)
+    return fail(DEIG_EWORKSPACE, "solver: workspace %zu bytes < required %zu", ws_bytes, total);
+  sv.op = op0;
+  sv.o = o;
+  sv.d = d;
+  sv.max_sweeps = max_sweeps;
+  sv.tol = tol;
+  sv.st = st;
+  const bool can_deflate = o.deflate && !op0.implicit && k >= 2;
+  double shift = 0.0;
+  float scale = 0.f;  // |theta| scale of the operator (first block's Ritz values)
+  bool all_conv = true;
+  float worst = 0.f;
+  int rc = DEIG_OK;
+  for (int attempt = 0;; ++attempt) {
+    all_conv = true;
+    worst = 0.f;
+    bool restart = false;
+    int locked = 0;     // pairs locked at V columns [k - locked, k)
+    bool redo = false;  // re-iterate the rest of a block after locking its dominant pairs
+    int warm = 0;       // redo: columns of the block computed before (just below locked)
+    while (locked < k) {
+      const int rem = k - locked;
+      const int kc = rem <= kb ? rem : kb;
+      // the last block of k > 128 pairs: the default subspace for its size
+      const int pb = (rem <= kb && k > kMaxP) ? std::min(default_subspace(d, kc), pb0) : pb0;
+      float* Vb = V + (int64_t)(k - locked - kc) * ldv;
+      float* evb = evals + (k - locked - kc);
+      sv.op.shift = shift;
+      sv.op.r = locked;
+      sv.op.Vd = locked ? V + (int64_t)(k - locked) * ldv : nullptr;
+      sv.op.ldvd = ldv;
+      sv.op.lamd = locked ? evals + (k - locked) : nullptr;
+      if ((rc = sv.prepare(pb))) break;
+      if (redo) {  // warm start: the block's columns below the dominant pairs
+        rc = rr_init_launch(sv.w.rr.Z, d, pb, V + (int64_t)(k - locked - warm) * ldv, warm, ldv,
+                            0x5eed5eefull + locked, st);
+      } else if (locked == 0 && k <= kMaxP) {
+        rc = rr_init_launch(sv.w.rr.Z, d, pb, Q0, k0, ldq0, 0x5eed5eedull, st);
+      } else {
+        rc = rr_init_launch(sv.w.rr.Z, d, pb, nullptr, 0, 0, 0x5eed5eedull + locked, st);
+      }
+      if (rc) break;
+      bool early = false;
+      const bool allow_early = can_deflate && o.deflate_early && !redo;
+      if ((rc = sv.iterate(kc, pb, Vb, ldv, evb, allow_early, &early))) break;
+      if (locked > 0 && (rc = deflate_orth_launch(Vb, ldv, d, kc, locked, st))) break;
+      if (locked == 0 && attempt == 0)
+        scale = fmaxf(fabsf(sv.lam_h[0]), fabsf(sv.lam_h[pb - 1]));
+      // Indefinite S: the most negative Ritz value of the block against the block's
+      // target (and the operator's scale - deflation residue is ~1e-7 of it).
+      const float tmin = sv.lam_h[pb - 1];
+      if (!op0.implicit && attempt < kMaxShifts &&
+          tmin < -fmaxf(kNegRel * scale, kNegTarget * fmaxf(sv.lam_h[kc - 1], 0.f))) {
+        shift = kShiftGrow * ((double)shift - (double)tmin);  // |theta_min| of the shifted op
+        if (o.debug)
+          fprintf(stderr, "[deig] negative Ritz value %.4e: restarting on S + %.4e I\n", tmin, shift);
+        restart = true;
+        break;
+      }
+      const int r = (can_deflate && !redo && (sv.converged || early)) ? sv.dominant(kc) : 0;
+      if (o.debug && r)
+        fprintf(stderr, "[deig] locking %d dominant pair(s)%s at sweep %d\n", r,
+                early ? " (early)" : "", sv.it);
+      if (r >= 1 && r < kc) {
+        locked += r;  // the rest of the block is iterated again (warm) below them
+        warm = kc - r;
+        redo = true;
+        continue;
+      }
+      worst = fmaxf(worst, sv.last);
+      if (!sv.converged) all_conv = false;
+      locked += kc;
+      redo = false;
     }
+    if (rc || !restart) break;
   }
-  if (sweeps_out) *sweeps_out = it;
-  if (resid_out) *resid_out = last;
-  if (!converged)
-    return fail(DEIG_NOT_CONVERGED, "solver: residual %g > tol %g after %d sweeps%s", last, tol,
-                it, it < max_sweeps ? " (stalled: eigengap at k too small for the subspace)" : "");
+  if (!rc && shift != 0.0) rc = unshift_launch(evals, k, shift, st);
+  if (sweeps_out) *sweeps_out = sv.it;
+  if (resid_out) *resid_out = rc ? sv.last : worst;
+  if (rc) return rc;
+  if (!all_conv)
+    return fail(DEIG_NOT_CONVERGED, "solver: residual %g > tol %g after %d sweeps%s", worst, tol,
+                sv.it, " (eigengap at k too small for the sweep budget, or stalled)");
   return DEIG_OK;
 }
 
@@ -490,9 +641,33 @@ using namespace deig;
 
 extern "C" {
 
-int deig_version(void) { return 0x000100; }
+int deig_version(void) { return 0x000300; }
 
 const char* deig_last_error(void) { return g_err; }
+
+void deig_solver_opts_init(deig_solver_opts* o) {
+  if (!o) return;
+  memset(o, 0, sizeof(*o));
+  o->size = (int)sizeof(deig_solver_opts);
+  o->sweep_algo = DEIG_SWEEP_AUTO;
+  o->rr_every = 0;
+  o->chebyshev = 1;
+  o->cheb_above = 1e-2f;
+  o->deflate = 1;
+  o->deflate_early = 1;
+  o->jacobi_early_sweeps = -1;
+  o->jacobi_early_above = -1.f;
+  o->fast_until = 1e-3f;
+  o->round_until = 1e-4f;
+  o->debug = 0;
+}
+
+static int check_opts(const deig_solver_opts* o) {
+  if (o && o->size != (int)sizeof(deig_solver_opts))
+    return fail(DEIG_EINVAL, "solver options: size %d != %d (call deig_solver_opts_init)", o->size,
+                (int)sizeof(deig_solver_opts));
+  return DEIG_OK;
+}
 
 static int syrk_resolve(int64_t n, int algo) {
   if (algo != DEIG_SYRK_AUTO) return algo;
@@ -526,6 +701,18 @@ int deig_syrk_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha
   return deig_syrk_f32_ex(X, n, d, ldx, alpha, S, lds, DEIG_SYRK_DEFAULT, ws, ws_bytes, stream);
 }
 
+size_t deig_syrk_shift_workspace(int64_t n, int64_t d, int xtype) {
+  return syrk_shift_workspace_bytes(n, d, xtype);
+}
+
+int deig_syrk_shift(const void* X, int xtype, int64_t n, int64_t d, int64_t ldx, double alpha,
+                    double* S64, int64_t lds64, float* S, int64_t lds, void* ws, size_t ws_bytes,
+                    void* stream) {
+  g_err[0] = 0;
+  return syrk_shift_launch(X, xtype, n, d, ldx, alpha, S64, lds64, S, lds, ws, ws_bytes,
+                           (hipStream_t)stream);
+}
+
 size_t deig_syrk_u8_workspace(int64_t n, int64_t d, int mode) {
   return syrk_u8_workspace_bytes(n, d, mode);
 }
@@ -538,58 +725,88 @@ int deig_syrk_u8(const uint8_t* X, int64_t n, int64_t d, int64_t ldx, int mode, 
                         (hipStream_t)stream);
 }
 
-int deig_default_subspace(int64_t d, int k) {
-  int64_t p = ((int64_t)k + (k < 16 ? 8 : k / 4) + 15) / 16 * 16;
-  if (p > kMaxP) p = kMaxP;
-  if (p > d) p = d / 16 * 16;
-  if (p < k) p = (k + 15) / 16 * 16;
-  return (int)p;
+int deig_default_subspace(int64_t d, int k) { return default_subspace(d, k); }
+
+static size_t topk_ws(int64_t d, int k, int p, bool implicit, int64_t mk, const deig_solver_opts* o) {
+  const Opts oo = make_opts(o);
+  int pb, kb;
+  block_shape(d, k, p, &pb, &kb);
+  if (pb < 16) pb = 16;
+  if (kb < 1) kb = 1;
+  const bool image = !implicit && oo.sweep_algo != DEIG_SWEEP_FP32;
+  size_t total = 0;
+  carve_solver(nullptr, 0, d, kb, k, pb, implicit ? mk : 0, image, &total);
+  return total;
 }
 
-size_t deig_topk_workspace(int64_t d, int k, int p) {
-  if (p <= 0) p = deig_default_subspace(d, k);
-  size_t total = 0;
-  carve_solver(nullptr, 0, d, k, p, 0, &total);
-  return total;
+size_t deig_topk_workspace_ex(int64_t d, int k, int p, int stype, const deig_solver_opts* opts) {
+  (void)stype;
+  return topk_ws(d, k, p, false, 0, opts);
+}
+
+size_t deig_topk_workspace(int64_t d, int k, int p) { return topk_ws(d, k, p, false, 0, nullptr); }
+
+int deig_topk_sym_ex(const void* S, int stype, int64_t d, int64_t lds, int k, int p, int max_sweeps,
+                     float tol, const float* Q0, int k0, int64_t ldq0, float* V, int64_t ldv,
+                     float* evals, int* sweeps_out, float* resid_out, const deig_solver_opts* opts,
+                     void* ws, size_t ws_bytes, void* stream) {
+  g_err[0] = 0;
+  if (int rc = check_opts(opts)) return rc;
+  if (stype != DEIG_F32 && stype != DEIG_F64)
+    return fail(DEIG_EINVAL, "topk: unknown element type %d", stype);
+  if (!S || lds < d || lds % 4 != 0 || !aligned16(S))
+    return fail(DEIG_EINVAL, "topk: S must be 16-byte aligned with lds >= d, lds %% 4 == 0");
+  Operator op{};
+  op.implicit = false;
+  op.S = S;
+  op.stype = stype;
+  op.lds = lds;
+  return solve(op, d, k, p, max_sweeps, tol, Q0, k0, ldq0, V, ldv, evals, sweeps_out, resid_out,
+               make_opts(opts), ws, ws_bytes, (hipStream_t)stream);
 }
 
 int deig_topk_sym_f32(const float* S, int64_t d, int64_t lds, int k, int p, int max_sweeps,
                       float tol, const float* Q0, int k0, int64_t ldq0, float* V, int64_t ldv,
                       float* evals, int* sweeps_out, float* resid_out, void* ws, size_t ws_bytes,
                       void* stream) {
-  g_err[0] = 0;
-  if (!S || lds < d || lds % 4 != 0 || !aligned16(S))
-    return fail(DEIG_EINVAL, "topk: S must be 16-byte aligned with lds >= d, lds %% 4 == 0");
-  Operator op{};
-  op.implicit = false;
-  op.S = S;
-  op.lds = lds;
-  return solve(op, d, k, p, max_sweeps, tol, Q0, k0, ldq0, V, ldv, evals, sweeps_out, resid_out,
-               ws, ws_bytes, (hipStream_t)stream);
+  return deig_topk_sym_ex(S, DEIG_F32, d, lds, k, p, max_sweeps, tol, Q0, k0, ldq0, V, ldv, evals,
+                          sweeps_out, resid_out, nullptr, ws, ws_bytes, stream);
+}
+
+size_t deig_projavg_workspace_ex(int64_t d, int64_t mk, int k, int p,
+                                 const deig_solver_opts* opts) {
+  return topk_ws(d, k, p, true, mk, opts);
 }
 
 size_t deig_projavg_workspace(int64_t d, int64_t mk, int k, int p) {
-  if (p <= 0) p = deig_default_subspace(d, k);
-  size_t total = 0;
-  carve_solver(nullptr, 0, d, k, p, mk, &total);
-  return total;
+  return topk_ws(d, k, p, true, mk, nullptr);
+}
+
+int deig_projavg_topk_ex(const float* Wt, int64_t d, int64_t mk, int64_t ldw, float scale, int k,
+                         int p, int max_sweeps, float tol, const float* Q0, int k0, int64_t ldq0,
+                         float* V, int64_t ldv, float* evals, int* sweeps_out, float* resid_out,
+                         const deig_solver_opts* opts, void* ws, size_t ws_bytes, void* stream) {
+  g_err[0] = 0;
+  if (int rc = check_opts(opts)) return rc;
+  if (!Wt || mk < 1 || ldw < d || ldw % 4 != 0 || !aligned16(Wt))
+    return fail(DEIG_EINVAL, "projavg: Wt must be 16-byte aligned, mk >= 1, ldw >= d, ldw %% 4 == 0");
+  Operator op{};
+  op.implicit = true;
+  op.stype = DEIG_F32;
+  op.Wt = Wt;
+  op.mk = mk;
+  op.ldw = ldw;
+  op.scale = scale;
+  return solve(op, d, k, p, max_sweeps, tol, Q0, k0, ldq0, V, ldv, evals, sweeps_out, resid_out,
+               make_opts(opts), ws, ws_bytes, (hipStream_t)stream);
 }
 
 int deig_projavg_topk_f32(const float* Wt, int64_t d, int64_t mk, int64_t ldw, float scale, int k,
                           int p, int max_sweeps, float tol, const float* Q0, int k0, int64_t ldq0,
                           float* V, int64_t ldv, float* evals, int* sweeps_out, float* resid_out,
                           void* ws, size_t ws_bytes, void* stream) {
-  g_err[0] = 0;
-  if (!Wt || mk < 1 || ldw < d || ldw % 4 != 0 || !aligned16(Wt))
-    return fail(DEIG_EINVAL, "projavg: Wt must be 16-byte aligned, mk >= 1, ldw >= d, ldw %% 4 == 0");
-  Operator op{};
-  op.implicit = true;
-  op.Wt = Wt;
-  op.mk = mk;
-  op.ldw = ldw;
-  op.scale = scale;
-  return solve(op, d, k, p, max_sweeps, tol, Q0, k0, ldq0, V, ldv, evals, sweeps_out, resid_out,
-               ws, ws_bytes, (hipStream_t)stream);
+  return deig_projavg_topk_ex(Wt, d, mk, ldw, scale, k, p, max_sweeps, tol, Q0, k0, ldq0, V, ldv,
+                              evals, sweeps_out, resid_out, nullptr, ws, ws_bytes, stream);
 }
 
 int deig_sym_power_f32(const float* S, int64_t d, int64_t lds, float* Q, int p, int64_t ldq,
@@ -606,7 +823,7 @@ int deig_sym_power_f32(const float* S, int64_t d, int64_t lds, float* Q, int p, 
     return fail(DEIG_EINVAL, "sym_power: algorithm %d has no fused chain (bf16x6 only)", algo);
   hipStream_t st = (hipStream_t)stream;
   if (!prepared) {
-    const int rc = sweep_prepare(S, d, lds, p, ws, ws_bytes, st);
+    const int rc = sweep_prepare(S, DEIG_F32, d, lds, p, ws, ws_bytes, st);
     if (rc) return rc;
   }
   SweepStep step{};
@@ -618,8 +835,7 @@ int deig_sym_power_f32(const float* S, int64_t d, int64_t lds, float* Q, int p, 
   step.tau = 0.f;
   step.next_mode = smode;
   for (int i = 0; i < steps; ++i) {
-    const int rc = sweep_apply(S, d, lds, Q, p, ldq, Y, ldy, 1.f, ws, ws_bytes, st, smode, &step,
-                               i > 0);
+    const int rc = sweep_apply(Q, d, p, ldq, Y, ldy, 1.f, ws, ws_bytes, st, smode, &step, i > 0);
     if (rc) return rc;
   }
   return DEIG_OK;
@@ -647,11 +863,11 @@ int deig_sym_apply_f32(const float* S, int64_t d, int64_t lds, const float* Q, i
   if (algo != DEIG_SWEEP_AUTO && algo != DEIG_SWEEP_BF16X6)
     return fail(DEIG_EINVAL, "sym_apply: unknown algorithm %d", algo);
   if (!prepared) {
-    const int rc = sweep_prepare(S, d, lds, p, ws, ws_bytes, (hipStream_t)stream);
+    const int rc = sweep_prepare(S, DEIG_F32, d, lds, p, ws, ws_bytes, (hipStream_t)stream);
     if (rc) return rc;
   }
-  return sweep_apply(S, d, lds, Q, p, ldq, Y, ldy, alpha, ws, ws_bytes, (hipStream_t)stream,
-                     smode, nullptr, kernel_only, kernel_only);
+  return sweep_apply(Q, d, p, ldq, Y, ldy, alpha, ws, ws_bytes, (hipStream_t)stream, smode,
+                     nullptr, kernel_only, kernel_only);
 }
 
 size_t deig_oja_workspace(int64_t b, int64_t d, int k) { return oja_workspace_bytes(b, d, k); }

@@ -73,6 +73,12 @@ size_t syrk_split_workspace_bytes(int64_t n, int64_t d);
 int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha, float* S,
                       int64_t lds, void* ws, size_t ws_bytes, hipStream_t stream);
 
+// Mean-shifted covariance of float samples (shift.hip); xtype DEIG_F32 / DEIG_F64.
+size_t syrk_shift_workspace_bytes(int64_t n, int64_t d, int xtype);
+int syrk_shift_launch(const void* X, int xtype, int64_t n, int64_t d, int64_t ldx, double alpha,
+                      double* S64, int64_t lds64, float* S, int64_t lds, void* ws, size_t ws_bytes,
+                      hipStream_t stream);
+
 // Exact uint8 covariance on int8 MFMA (syrk_u8.hip); mode DEIG_U8_RAW / DEIG_U8_GRAY3.
 size_t syrk_u8_workspace_bytes(int64_t n, int64_t d, int mode);
 int syrk_u8_launch(const uint8_t* X, int64_t n, int64_t d, int64_t ldx, int mode, double alpha,
@@ -91,17 +97,13 @@ int skinny_launch(bool trans_a, const float* A, int64_t lda, const float* B, int
 // bf16x6 symmetric sweep (sweep.hip): Y = alpha * S Q, S symmetric d x d
 // row-major, Q d x p (ldq), Y d x p (ldy), p % 16 == 0, p <= 128.
 size_t sweep_workspace_bytes(int64_t d, int p);
-int sweep_launch(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
-                 float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st);
-// The same in two parts: sweep_prepare builds the S image in the workspace (once
-// per S), sweep_apply runs one product from it (S is still passed: the v1 kernel
-// reads it in place).
-// Vd / ldv / lamd / r (optional): the image is of S - Vd diag(lamd) Vd^T (r columns).
-int sweep_prepare(const float* S, int64_t d, int64_t lds, int p, void* ws, size_t ws_bytes,
-                  hipStream_t st, const float* Vd = nullptr, int64_t ldv = 0,
-                  const float* lamd = nullptr, int r = 0);
-// 1 = the row-major v1 sweep (reads S in place, no image, no deflation).
-int sweep_version();
+// sweep_prepare builds the image of  S + shift I - Vd diag(lamd) Vd^T  in the
+// workspace (once per operator; stype DEIG_F32 / DEIG_F64; the shift and the r
+// deflated pairs - Vd column-major, ldv - are formed in double), sweep_apply runs
+// one product from it.
+int sweep_prepare(const void* S, int stype, int64_t d, int64_t lds, int p, void* ws,
+                  size_t ws_bytes, hipStream_t st, const float* Vd = nullptr, int64_t ldv = 0,
+                  const float* lamd = nullptr, int r = 0, double shift = 0.0);
 // mode 0: exact (six products).  mode 1 (round_q): the solver's in-place mode - Q
 // (which must then be writable) is rounded to 16 significant bits (Q' = h + m, two
 // bf16 pieces) and the product S Q' formed with five bf16 products instead of six
@@ -125,9 +127,9 @@ struct SweepStep {
   float thr, a, cc, gamma;  // Chebyshev: X_{j+1} = a (Y - cc X_j) - gamma X_{j-1} if lam_j >= thr
   int next_mode;            // kSweep* of the next sweep
 };
-int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
-                float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st,
-                int mode = kSweepExact, const SweepStep* step = nullptr, bool q_ready = false,
+int sweep_apply(const float* Q, int64_t d, int p, int64_t ldq, float* Y, int64_t ldy, float alpha,
+                void* ws, size_t ws_bytes, hipStream_t st, int mode = kSweepExact,
+                const SweepStep* step = nullptr, bool q_ready = false,
                 bool kernel_only = false);  // kernel_only: no split-K reduction (measurement)
 
 // Rayleigh-Ritz pieces (rr.hip).
@@ -159,6 +161,8 @@ int rr_update_launch(const RRBuffers& b, int64_t d, int p, int k, float* V, int6
                      float* evals, hipStream_t stream);
 // Columns 0..kc-1 of V (col-major, ldv) made orthogonal to columns kc..kc+r-1, normalised.
 int deflate_orth_launch(float* V, int64_t ldv, int64_t d, int kc, int r, hipStream_t stream);
+// evals[0..k) -= shift (device).
+int unshift_launch(float* evals, int k, double shift, hipStream_t stream);
 
 // Oja (oja.hip).
 size_t oja_workspace_bytes(int64_t b, int64_t d, int k);

@@ -611,50 +611,64 @@ __global__ __launch_bounds__(256) void cheb_step_kernel(float* __restrict__ Z,
   *zq = xn;
 }
 
-// After the deflated stage (capi.hip): V_j <- normalize(V_j - V_D V_D^T V_j) for the kc
-// stage-2 columns against the r deflated ones (V_D = columns kc .. kc + r - 1).  The
-// deflated operator S - lam_1 v^ v^T keeps a coupling lam_1 (v_1 d^T + d v_1^T) from
-// the small error d = v^ - v_1, which tilts each remaining eigenvector towards v_1
-// by lam_1 d_j / lam_j; the span of [V, V_D] is right, and projecting v^ out is
-// exact to O(lam_1 |d|^2).  One block per column; fixed-order block reductions.
+// After a deflated stage or block (capi.hip): V_j <- normalize(V_j - V_D V_D^T V_j)
+// for the kc columns of the stage against the r locked ones (V_D = columns kc ..
+// kc + r - 1).  The deflated operator S - lam_1 v^ v^T keeps a coupling
+// lam_1 (v_1 d^T + d v_1^T) from the small error d = v^ - v_1, which tilts each
+// remaining eigenvector towards v_1 by lam_1 d_j / lam_j; the span of [V, V_D] is
+// right, and projecting v^ out is exact to O(lam_1 |d|^2).  One block per column;
+// V_D in chunks of 8 columns (modified Gram-Schmidt by chunk, twice when r > 8:
+// block locking of k > 128 pairs); fixed-order block reductions.
 __global__ __launch_bounds__(256) void deflate_orth_kernel(float* __restrict__ V, int64_t ldv,
                                                            int64_t d, int kc, int r) {
   __shared__ float red[4][8];
   __shared__ float coef[8];
   const int j = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   float* v = V + (int64_t)j * ldv;
-  const float* vd = V + (int64_t)kc * ldv;
-  float dot[8];
+  const float* vd0 = V + (int64_t)kc * ldv;
+  const int passes = r > 8 ? 2 : 1;
+  for (int pass = 0; pass < passes; ++pass)
+    for (int q0 = 0; q0 < r; q0 += 8) {
+      const int nq = r - q0 < 8 ? r - q0 : 8;
+      const float* vd = vd0 + (int64_t)q0 * ldv;
+      float dot[8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) dot[q] = 0.f;
-  for (int64_t i = tid; i < d; i += 256) {
-    const float x = v[i];
+      for (int q = 0; q < 8; ++q) dot[q] = 0.f;
+      for (int64_t i = tid; i < d; i += 256) {
+        const float x = v[i];
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
-      if (q < r) dot[q] = fmaf(vd[(int64_t)q * ldv + i], x, dot[q]);
-  }
+        for (int q = 0; q < 8; ++q)
+          if (q < nq) dot[q] = fmaf(vd[(int64_t)q * ldv + i], x, dot[q]);
+      }
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    float t = dot[q];
-    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-    if (lane == 0) red[w][q] = t;
-  }
-  __syncthreads();
-  if (tid < 8) coef[tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
-  __syncthreads();
+      for (int q = 0; q < 8; ++q) {
+        float t = dot[q];
+        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+        if (lane == 0) red[w][q] = t;
+      }
+      __syncthreads();
+      if (tid < 8) coef[tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+      __syncthreads();
+      for (int64_t i = tid; i < d; i += 256) {
+        float x = v[i];
+        for (int q = 0; q < nq; ++q) x = fmaf(-coef[q], vd[(int64_t)q * ldv + i], x);
+        v[i] = x;
+      }
+      __syncthreads();  // red / coef are reused by the next chunk
+    }
   float nrm = 0.f;
-  for (int64_t i = tid; i < d; i += 256) {
-    float x = v[i];
-    for (int q = 0; q < r; ++q) x = fmaf(-coef[q], vd[(int64_t)q * ldv + i], x);
-    v[i] = x;
-    nrm = fmaf(x, x, nrm);
-  }
+  for (int64_t i = tid; i < d; i += 256) nrm = fmaf(v[i], v[i], nrm);
   for (int o = 32; o > 0; o >>= 1) nrm += __shfl_xor(nrm, o, 64);
-  __syncthreads();
   if (lane == 0) red[w][0] = nrm;
   __syncthreads();
   const float sc = rsqrtf(red[0][0] + red[1][0] + red[2][0] + red[3][0]);
   for (int64_t i = tid; i < d; i += 256) v[i] *= sc;
+}
+
+// evals[j] -= shift (the solver's indefinite-input shift, undone at the end).
+__global__ void unshift_kernel(float* __restrict__ evals, int k, double shift) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j < k) evals[j] = (float)((double)evals[j] - shift);
 }
 
 size_t rr_small_shm(int p) {
@@ -675,36 +689,16 @@ int rr_init_launch(float* Z, int64_t d, int p, const float* Q0, int k0, int64_t 
 int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream, int max_jsweeps, float jrel) {
   DEIG_REQUIRE(p >= 4 && p <= 128 && p % 4 == 0, "rr_small: p=%d out of range", p);
   const size_t shm = rr_small_shm(p);
-  static bool attr = false;
-  if (!attr) {
-    DEIG_HIP_CHECK(hipFuncSetAttribute((const void*)rr_small_kernel<RT>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)rr_small_shm(128)));
-    DEIG_HIP_CHECK(hipFuncSetAttribute((const void*)rr_small_kernel<256>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)rr_small_shm(64)));
-    DEIG_HIP_CHECK(hipFuncSetAttribute((const void*)rr_small_kernel<64>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)rr_small_shm(32)));
-    attr = true;
-  }
+  // once per process (C++11 thread-safe static initialisation)
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)rr_small_kernel<RT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (int)rr_small_shm(128));
+  DEIG_HIP_CHECK(attr);
   // Workgroup size: 1024 threads at every p.  Each Jacobi step is a chain of LDS
   // round trips per thread, so the most threads (shortest per-thread chain) win:
   // measured r02 at p = 32, Jacobi 75 us (1024) vs 89 (256) vs 184 (64) per RR.
-  // DEIG_RR_THREADS=64|256 selects the narrower builds for such comparisons.
-  static const int nt_env = getenv("DEIG_RR_THREADS") ? atoi(getenv("DEIG_RR_THREADS")) : 0;
-  int nt = RT;
-  if (nt_env == 64 && p <= 32) nt = 64;
-  if (nt_env == 256 && p <= 64) nt = 256;
-  if (nt == 64)
-    hipLaunchKernelGGL(rr_small_kernel<64>, dim3(1), dim3(64), shm, stream, b.C, p, b.W, b.lam,
-                       b.cs, b.qs, b.info, max_jsweeps, jrel);
-  else if (nt == 256)
-    hipLaunchKernelGGL(rr_small_kernel<256>, dim3(1), dim3(256), shm, stream, b.C, p, b.W, b.lam,
-                       b.cs, b.qs, b.info, max_jsweeps, jrel);
-  else
-    hipLaunchKernelGGL(rr_small_kernel<RT>, dim3(1), dim3(RT), shm, stream, b.C, p, b.W, b.lam,
-                       b.cs, b.qs, b.info, max_jsweeps, jrel);
+  hipLaunchKernelGGL(rr_small_kernel<RT>, dim3(1), dim3(RT), shm, stream, b.C, p, b.W, b.lam, b.cs,
+                     b.qs, b.info, max_jsweeps, jrel);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }
@@ -726,8 +720,15 @@ int cheb_step_launch(const RRBuffers& b, float* T, int64_t d, int p, float thr, 
 }
 
 int deflate_orth_launch(float* V, int64_t ldv, int64_t d, int kc, int r, hipStream_t stream) {
-  DEIG_REQUIRE(r >= 1 && r <= 8 && kc >= 1, "deflate_orth: r=%d kc=%d out of range", r, kc);
+  DEIG_REQUIRE(r >= 1 && kc >= 1, "deflate_orth: r=%d kc=%d out of range", r, kc);
   hipLaunchKernelGGL(deflate_orth_kernel, dim3(kc), dim3(256), 0, stream, V, ldv, d, kc, r);
+  DEIG_HIP_CHECK(hipGetLastError());
+  return DEIG_OK;
+}
+
+int unshift_launch(float* evals, int k, double shift, hipStream_t stream) {
+  hipLaunchKernelGGL(unshift_kernel, dim3((unsigned)cdiv(k, 256)), dim3(256), 0, stream, evals, k,
+                     shift);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }
@@ -739,13 +740,10 @@ int rr_update_launch(const RRBuffers& b, int64_t d, int p, int k, float* V, int6
   const int nblk = rr_update_blocks(d);
   DEIG_REQUIRE(p >= 16 && p <= 128, "rr_update: p=%d out of range", p);
   const size_t shm = (size_t)(p * p + UR * 2 * p + (256 / p) * k) * sizeof(float);
-  static bool attr = false;
-  if (!attr) {
-    DEIG_HIP_CHECK(hipFuncSetAttribute((const void*)rr_update_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)((128 * 128 + UR * 256 + 16 * 128) * sizeof(float))));
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)rr_update_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (int)((128 * 128 + UR * 256 + 16 * 128) * sizeof(float)));
+  DEIG_HIP_CHECK(attr);
   hipLaunchKernelGGL(rr_update_kernel, dim3(nblk), dim3(256), shm, stream, b.Z, d, p, k, b.W,
                      b.lam, b.cs, b.qs, V, ldv, b.resid_part);
   DEIG_HIP_CHECK(hipGetLastError());

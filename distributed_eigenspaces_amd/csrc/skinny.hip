@@ -193,12 +193,10 @@ int launch_nb(const float* A, int64_t lda, const float* B, int64_t ldb, float* C
               hipStream_t st) {
   constexpr int N = NB * 16;
   const size_t shm = (size_t)(2 * SBK * AST + 2 * SBK * bstride(N)) * sizeof(float);
-  static bool attr_set = false;  // benign race: idempotent attribute
-  if (!attr_set) {
-    DEIG_HIP_CHECK(hipFuncSetAttribute((const void*)skinny_kernel<NB, TRANS>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-    attr_set = true;
-  }
+  // once per instantiation (C++11 thread-safe static initialisation)
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)skinny_kernel<NB, TRANS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  DEIG_HIP_CHECK(attr);
   dim3 grid((unsigned)cdiv(M, SBM), (unsigned)ks);
   hipLaunchKernelGGL((skinny_kernel<NB, TRANS>), grid, dim3(ST), shm, st, A, lda, B, ldb, C, ldc,
                      M, K, alpha, beta, part);
@@ -225,20 +223,13 @@ int launch_t(int NB, const float* A, int64_t lda, const float* B, int64_t ldb, f
 
 // Split-K factor: enough blocks for ~4 resident per CU (latency hiding: HBM
 // latency under load is ~1-2 us, one chunk of MFMA work ~0.5 us), >= 8 chunks
-// per slice.  DEIG_SKINNY_BPC overrides the blocks-per-CU target (tuning).
-int blocks_per_cu() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DEIG_SKINNY_BPC");
-    v = (e && atoi(e) > 0) ? atoi(e) : 4;
-  }
-  return v;
-}
+// per slice.
+constexpr int kBlocksPerCu = 4;
 
 int choose_ks(int64_t M, int64_t K) {
   const int64_t mb = cdiv(M, SBM);
   const int64_t nch = cdiv(K, SBK);
-  int64_t ks = cdiv((int64_t)blocks_per_cu() * num_cus(), mb);
+  int64_t ks = cdiv((int64_t)kBlocksPerCu * num_cus(), mb);
   const int64_t cap = nch / 8 > 1 ? nch / 8 : 1;
   if (ks > cap) ks = cap;
   if (ks < 1) ks = 1;

@@ -16,25 +16,11 @@
 // at 157 TF/s) for p <= 128.
 //
 // Y[m][:] = sum_k S[m][k] Q[k][:]  (S = S^T, so ROWS of S are read, contiguous
-// along k).  v_mfma_f32_16x16x32_bf16: lane l holds A[m = l%16][k = 8(l/16)..+7]
-// - 32 contiguous bytes of one row of S, loaded straight into registers, no LDS
-// - and B[k = 8(l/16)..+7][n = l%16] from the Q image, staged through LDS once
-// per block and K-step and shared by the 8 waves.  Block = 8 waves x 32 rows (2
-// MFMA row blocks per wave, all p columns); K-step = 64 (2 MFMA k-groups) with
-// two register stages of the S rows and of the Q stage.  Split-K over ks
-// slices (XCD-aware block order); partial slabs are summed in slice order
-// (deterministic).
-//
-// Measured (d = 8192, p = 80, rocprofv3, one MI355X): 90 us per launch (+4 us
-// split_q, +6 us reduce) = 3.0 TB/s of S.  Attribution by knock-out builds of
-// the same kernel: without S loads 64 us, without MFMAs 84 us, without both 36 us
-// (Q-stage loads/LDS stores 15 us of it, the split 10 us); S read as one
-// contiguous 8 KiB run per wave-step instead of 32 rows x 256 B: -11 us.  The
-// phases add rather than overlap (the per-step barrier keeps the 8 waves in
-// lock-step), so the next lever is a staggered / warp-specialised schedule, not
-// more bandwidth.
-#include <stdlib.h>
-
+// along k).  S is re-laid once per solve into an image in MFMA A-operand order
+// (sweep_prepare_kernel), which the sweep kernels stream as one contiguous run per
+// wave (v2: independent waves, Q fragments in registers; v3: the Q image shared
+// through an LDS-DMA ring).  Split-K over an XCD-aware grid; slabs summed in slice
+// order (deterministic), fused with the solver's basis step (sweep_finish_kernel).
 #include <type_traits>
 
 #include "deig_internal.hpp"
@@ -45,9 +31,7 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int SW_THR = 512;   // 8 waves
-constexpr int SW_ROWS = 256;  // rows per block: 8 waves x 2 x 16
-constexpr int SW_KS = 64;     // k per stage
+constexpr int SW_KS = 64;  // k per sweep step (two 32-deep MFMA k-groups)
 
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -122,161 +106,6 @@ __global__ __launch_bounds__(256) void split_q_kernel(float* __restrict__ Q, int
   }
 }
 
-template <int NB>
-__global__ __launch_bounds__(SW_THR) void sweep_kernel(const float* __restrict__ S, int64_t lds,
-                                                       int64_t d, const u32x4* __restrict__ QS,
-                                                       int64_t nsteps, float* __restrict__ Y,
-                                                       int64_t ldy, float alpha,
-                                                       float* __restrict__ part) {
-  constexpr int BV = 2 * NB * 3 * 64;  // 16-B units of one Q stage (2 k-groups)
-  constexpr int BPT = (BV + SW_THR - 1) / SW_THR;
-  __shared__ u32x4 Bs[2][BV];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 15, gq = lane >> 4;
-  // 1-D grid of bx row blocks x ks split-K slices, XCD-aware: consecutive logical
-  // ids (one XCD) take consecutive row blocks of ONE slice, so an XCD's L2 holds
-  // only that slice's part of the Q image.
-  const int bx = (int)cdiv(d, SW_ROWS);
-  const int ks = (int)(gridDim.x / bx);
-  const int lid = xcd_logical(blockIdx.x, gridDim.x);
-  const int sl = lid / bx;
-  const int64_t row0 = (int64_t)(lid - sl * bx) * SW_ROWS + 32 * wave;
-  const int64_t c0 = nsteps * sl / ks, c1 = nsteps * (sl + 1) / ks;
-
-  f32x4 acc[2][NB];
-#pragma unroll
-  for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-    for (int j = 0; j < NB; ++j) acc[mb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // Two register stages of raw fp32 S rows ([stage][m-block][k-group][half]) and
-  // of the Q image: S(s + 2) and Q(s + 2) are issued while step s computes, S
-  // before Q, so the in-order vmcnt wait for Q(s + 1) (needed by its LDS store at
-  // the end of step s) leaves S(s + 2) in flight - about two steps of latency
-  // cover instead of none (__syncthreads() would wait for everything).
-  f32x4 ra[2][2][2][2];
-  u32x4 rq[2][BPT];
-
-  // S rows through a per-wave buffer descriptor over this wave's 32 rows: one
-  // straight-line 16-B load per operand half, no branches (a divergent branch
-  // makes the compiler wait for every outstanding load).  Rows >= d read as 0
-  // (range check); columns >= d are zeroed when the step is consumed.
-  const int64_t wrows = d - row0 < 32 ? (d - row0 > 0 ? d - row0 : 0) : 32;
-  const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(S + (row0 < d ? row0 : 0) * lds), 0, (int)(wrows * lds * 4), 0x00020000);
-  auto load_a = [&](f32x4 (&dst)[2][2][2], int64_t step) {
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-      for (int g = 0; g < 2; ++g)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int off = (int)(((16 * mb + r) * lds + step * SW_KS + 32 * g + 8 * gq + 4 * h) * 4);
-          dst[mb][g][h] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(srs, off, 0, 0));
-        }
-  };
-  auto mask_cols = [&](f32x4 (&v)[2][2][2], int64_t step) {
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-      for (int g = 0; g < 2; ++g)
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (step * SW_KS + 32 * g + 8 * gq + 4 * h + e >= d) v[mb][g][h][e] = 0.f;
-  };
-  auto load_q = [&](u32x4 (&dst)[BPT], int64_t step) {
-#pragma unroll
-    for (int u = 0; u < BPT; ++u) {
-      const int f = tid + u * SW_THR;
-      dst[u] = QS[step * BV + (f < BV ? f : BV - 1)];  // lanes past BV are not stored
-    }
-  };
-  auto store_q = [&](const u32x4 (&src)[BPT], int buf) {
-#pragma unroll
-    for (int u = 0; u < BPT; ++u) {
-      const int f = tid + u * SW_THR;
-      if (f < BV) Bs[buf][f] = src[u];
-    }
-  };
-  auto barrier = [&]() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-  // Step `step` with its S rows in ra[B] and its Q stage in Bs[B].
-  auto body = [&](auto Bc, int64_t step) {
-    constexpr int B = decltype(Bc)::value;
-    u32x4 ah[2][2], am[2][2], al[2][2];
-    if ((step + 1) * SW_KS > d) mask_cols(ra[B], step);  // wave-uniform, last step only
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-      for (int g = 0; g < 2; ++g)
-        split8(ra[B][mb][g][0], ra[B][mb][g][1], ah[mb][g], am[mb][g], al[mb][g]);
-    // Unconditional (the last two steps re-load the last step: straight-line
-    // code, no phi copies of in-flight registers).
-    const int64_t pf = step + 2 < c1 ? step + 2 : c1 - 1;
-    load_a(ra[B], pf);
-    load_q(rq[B], pf);
-    __builtin_amdgcn_sched_barrier(0);  // issue the loads here, ahead of the MFMAs
-#pragma unroll
-    for (int g = 0; g < 2; ++g)
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const u32x4 bh = Bs[B][((g * NB + j) * 3 + 0) * 64 + lane];
-        const u32x4 bm = Bs[B][((g * NB + j) * 3 + 1) * 64 + lane];
-        const u32x4 bl = Bs[B][((g * NB + j) * 3 + 2) * 64 + lane];
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {  // small terms first
-          acc[mb][j] = mfma16(am[mb][g], bm, acc[mb][j]);
-          acc[mb][j] = mfma16(ah[mb][g], bl, acc[mb][j]);
-          acc[mb][j] = mfma16(al[mb][g], bh, acc[mb][j]);
-          acc[mb][j] = mfma16(ah[mb][g], bm, acc[mb][j]);
-          acc[mb][j] = mfma16(am[mb][g], bh, acc[mb][j]);
-          acc[mb][j] = mfma16(ah[mb][g], bh, acc[mb][j]);
-        }
-      }
-    // Bs[B ^ 1] was last read in step - 1, before the previous barrier.
-    store_q(rq[B ^ 1], B ^ 1);  // Q(step + 1) (after the last step: unread)
-    barrier();
-  };
-
-  if (c0 < c1) {
-    const int64_t c01 = c0 + 1 < c1 ? c0 + 1 : c0;
-    load_a(ra[0], c0);
-    load_q(rq[0], c0);
-    load_a(ra[1], c01);
-    load_q(rq[1], c01);
-    store_q(rq[0], 0);
-    barrier();
-    int64_t step = c0;
-    for (; step + 1 < c1; step += 2) {
-      body(std::integral_constant<int, 0>{}, step);
-      body(std::integral_constant<int, 1>{}, step + 1);
-    }
-    if (step < c1) body(std::integral_constant<int, 0>{}, step);
-  }
-
-  // C/D layout of 16x16x32: row 4 (l / 16) + e, column l % 16
-  constexpr int P = 16 * NB;
-#pragma unroll
-  for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-    for (int j = 0; j < NB; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int64_t row = row0 + 16 * mb + 4 * gq + e;
-        if (row < d) {
-          if (ks == 1)
-            Y[row * ldy + 16 * j + r] = alpha * acc[mb][j][e];
-          else
-            part[((int64_t)sl * d + row) * P + 16 * j + r] = acc[mb][j][e];
-        }
-      }
-}
-
 // The products of one Q fragment (pieces bh, bm[, bl]) with MB split S
 // fragments into column block j, small terms first, MB independent accumulators
 // between dependent MFMAs.  NP = 3: hh + hm + mh + hl + lh + mm (six); NP = 2
@@ -331,23 +160,27 @@ __host__ __device__ inline int64_t si_rows(int64_t d) { return cdiv(d, SI_BR) * 
 __host__ __device__ inline int64_t si_groups(int64_t d) { return cdiv(d, 32); }
 size_t si_bytes(int64_t d) { return (size_t)si_rows(d) * si_groups(d) * 32 * 4; }
 
-// One thread per (rb, g, mb, lane): reads 32 contiguous bytes of one row, writes
-// the two 16-B halves (h = 0, 1) 1 KiB apart (d = 8192: 88 us = 6.1 TB/s of
-// read + write; an LDS-transposed variant with whole-row reads took 131 us).
-// Optional deflation (the eigensolver's second stage, capi.hip): the image is of
-// S - V_D diag(lam_D) V_D^T for r dominant eigenpairs (V_D column-major, ldv),
-// formed in fp32 with one fma per pair and element: the deflated entries then carry
-// about the rounding error of S itself, so products with the image no longer lose
-// the small eigenvalues' digits to cancellation against the dominant ones.
-__global__ __launch_bounds__(256) void sweep_prepare_kernel(const float* __restrict__ S,
-                                                            int64_t lds, int64_t d, int64_t ng,
-                                                            int64_t nunits,
+// One thread per (rb, g, mb, lane): reads 32 contiguous bytes of one row (64 for
+// a float64 S), writes the two 16-B halves (h = 0, 1) 1 KiB apart (d = 8192: 88 us
+// = 6.1 TB/s of read + write; an LDS-transposed variant with whole-row reads took
+// 131 us).  The image is of
+//   S + shift I - V_D diag(lam_D) V_D^T
+// with the shift and the optional deflation (r locked / dominant eigenpairs, V_D
+// column-major with ldv) formed in DOUBLE from S's own values and rounded to fp32
+// once: the deflated entries then carry fp32 rounding relative to THEIR size, not
+// to the dominant eigenvalues' (for a float64 S - the reference's dtype - this is
+// what keeps the small eigenvectors at float64 parity; an fp32 chain of fmas
+// would round every intermediate at |S_ij|).  shift: the solver's indefinite-input
+// shift (capi.hip), 0 otherwise.
+template <typename T>
+__global__ __launch_bounds__(256) void sweep_prepare_kernel(const T* __restrict__ S, int64_t lds,
+                                                            int64_t d, int64_t ng, int64_t nunits,
                                                             f32x4* __restrict__ SI,
                                                             u32x4* __restrict__ SH,
                                                             const float* __restrict__ Vd,
                                                             int64_t ldv,
-                                                            const float* __restrict__ lamd,
-                                                            int r) {
+                                                            const float* __restrict__ lamd, int r,
+                                                            double shift) {
   const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (u >= nunits) return;
   const int lane = (int)(u & 63);
@@ -358,24 +191,34 @@ __global__ __launch_bounds__(256) void sweep_prepare_kernel(const float* __restr
   const int64_t k = 32 * g + 8 * (lane >> 4);
   f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = {0.f, 0.f, 0.f, 0.f};
   if (row < d) {
-    const float* src = S + row * lds + k;
-    if (k + 8 <= d) {
-      v0 = *reinterpret_cast<const f32x4*>(src);
-      v1 = *reinterpret_cast<const f32x4*>(src + 4);
-    } else {
+    const T* src = S + row * lds + k;
+    if (r == 0 && shift == 0.0 && std::is_same<T, float>::value) {  // plain copy
+      if (k + 8 <= d) {
+        v0 = *reinterpret_cast<const f32x4*>(src);
+        v1 = *reinterpret_cast<const f32x4*>(src + 4);
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (k + e < d) v0[e] = src[e];
-        if (k + 4 + e < d) v1[e] = src[4 + e];
+        for (int e = 0; e < 4; ++e) {
+          if (k + e < d) v0[e] = (float)src[e];
+          if (k + 4 + e < d) v1[e] = (float)src[4 + e];
+        }
       }
-    }
-    for (int q = 0; q < r; ++q) {
-      const float* vq = Vd + (int64_t)q * ldv;
-      const float a = -lamd[q] * vq[row];
+    } else {
+      double v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (k + e < d) ? (double)src[e] : 0.0;
+      if (row >= k && row < k + 8) v[row - k] += shift;
+      for (int q = 0; q < r; ++q) {
+        const float* vq = Vd + (int64_t)q * ldv;
+        const double a = -(double)lamd[q] * (double)vq[row];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (k + e < d) v[e] = fma(a, (double)vq[k + e], v[e]);
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        if (k + e < d) v0[e] = fmaf(a, vq[k + e], v0[e]);
-        if (k + 4 + e < d) v1[e] = fmaf(a, vq[k + 4 + e], v1[e]);
+        v0[e] = (float)v[e];
+        v1[e] = (float)v[4 + e];
       }
     }
   }
@@ -402,8 +245,8 @@ __global__ __launch_bounds__(256) void sweep_prepare_kernel(const float* __restr
 // bytes as S from HBM (1.9x at p = 80), but there is no block-wide lock-step:
 // the four waves of a CU (one per SIMD, up to 512 registers each) stream
 // independently, each with a D-deep register ring of S and Q fragments.
-// PROBE (diagnostic builds only, DEIG_SWEEP_PROBE): bit 0 drops the MFMAs, bit 1
-// the S loads, bit 2 the Q loads (results are then garbage).
+// PROBE (knock-out builds for attribution, never launched by the library): bit 0
+// drops the MFMAs, bit 1 the S loads, bit 2 the Q loads (results are garbage).
 // PRE: SI is the two-piece image (sweep_prepare_kernel's SH: h | m per half slot)
 // and the products are the three of SP = 2 - the early-sweep mode, no split.
 template <int NB, int NP, int PROBE = 0, bool PRE = false>
@@ -806,19 +649,11 @@ __global__ __launch_bounds__(256) void sweep_finish_kernel(const float* __restri
   }
 }
 
-int sweep_bpc() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DEIG_SWEEP_BPC");
-    v = (e && atoi(e) > 0) ? atoi(e) : 1;
-  }
-  return v;
-}
-
-// Split-K slices: about sweep_bpc() blocks per CU, >= 4 K-steps per slice.
+// Split-K slices: about one block per CU, >= 4 K-steps per slice (r01g: two
+// blocks per CU and finer slices measured slower).
 int sweep_ks(int64_t d) {
-  const int64_t bx = cdiv(d, SW_ROWS), nsteps = cdiv(d, SW_KS);
-  int64_t ks = cdiv((int64_t)num_cus() * sweep_bpc(), bx);
+  const int64_t bx = cdiv(d, SI_BR), nsteps = cdiv(d, SW_KS);
+  int64_t ks = cdiv((int64_t)num_cus(), bx);
   const int64_t cap = nsteps / 4 > 1 ? nsteps / 4 : 1;
   if (ks > cap) ks = cap;
   if (ks < 1) ks = 1;
@@ -831,22 +666,15 @@ int sweep_ks(int64_t d) {
 // 47.9, per sweep in the chain 52.4 vs 58.0), else 4 (p = 128: 272 vs 249 us per
 // sweep - there the Q fragment reuse of 64-row waves wins; with the split in the
 // sweep no gain either).  Ring depths 5-8 measured the same as 3
-// (profiles/r02n_sweep_mb.log).  DEIG_SWEEP_MB=2|4 overrides.
-int sweep_mb(bool pre, int nb) {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DEIG_SWEEP_MB");
-    v = (e && (atoi(e) == 2 || atoi(e) == 4)) ? atoi(e) : 0;
-  }
-  if (v) return v;
-  return (pre && nb <= 5) ? 2 : 4;
-}
+// (profiles/r02n_sweep_mb.log), so the ring is 3 deep.
+int sweep_mb(bool pre, int nb) { return (pre && nb <= 5) ? 2 : 4; }
+constexpr int kSweepDepth = 3;
 
 // Split-K slices of a v3 launch with mb m-blocks per wave (rows per block 64 mb).
 int sweep_ks_mb(int64_t d, int mb) {
   if (mb == 4) return sweep_ks(d);
   const int64_t bx = cdiv(d, 64 * mb), nsteps = cdiv(d, SW_KS);
-  int64_t ks = cdiv((int64_t)num_cus() * sweep_bpc(), bx);
+  int64_t ks = cdiv((int64_t)num_cus(), bx);
   const int64_t cap = nsteps / 4 > 1 ? nsteps / 4 : 1;
   if (ks > cap) ks = cap;
   if (ks < 1) ks = 1;
@@ -857,101 +685,24 @@ int sweep_ks_mb(int64_t d, int mb) {
 // Q image: 3 bf16 pieces per value
 size_t qs_bytes(int64_t d, int p) { return (size_t)cdiv(d, SW_KS) * SW_KS * p * 6; }
 
-// Kernel version: 0 = default (v2 for p <= 80, v3 above, where v2's register
-// rings spill), 2 (S image, independent waves with Q in registers), 3 (S image,
-// LDS-shared Q ring) or 1 (row-major S, register-staged Q stage, 8 waves);
-// DEIG_SWEEP_KERNEL selects one, for A/B timing.
-}  // namespace
-
-int sweep_version() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DEIG_SWEEP_KERNEL");
-    v = (e && atoi(e) >= 1 && atoi(e) <= 3) ? atoi(e) : 0;
-  }
-  return v;
-}
-
-namespace {
-
-template <int NB>
-void launch_v1(dim3 grid, hipStream_t st, const float* S, int64_t lds, int64_t d, const u32x4* QS,
-               float* Y, int64_t ldy, float alpha, float* part) {
-  hipLaunchKernelGGL(sweep_kernel<NB>, grid, dim3(SW_THR), 0, st, S, lds, d, QS, cdiv(d, SW_KS),
-                     Y, ldy, alpha, part);
-}
-
 template <int NB, int NP, bool PRE>
 void launch_v2(dim3 grid, hipStream_t st, const f32x4* SI, int64_t d, const u32x4* QS, float* Y,
                int64_t ldy, float alpha, float* part) {
   const int64_t ng = si_groups(d);
-  if constexpr (PRE) {
-    hipLaunchKernelGGL((sweep2_kernel<NB, NP, 0, true>), grid, dim3(256), 0, st, SI, d, QS, ng, Y,
-                       ldy, alpha, part);
-    return;
-  }
-  if constexpr (NB == 5 && NP == 3) {
-    static const int probe = getenv("DEIG_SWEEP_PROBE") ? atoi(getenv("DEIG_SWEEP_PROBE")) : 0;
-    switch (probe) {
-#define DEIG_PROBE_CASE(P_)                                                                   \
-  case P_:                                                                                   \
-    hipLaunchKernelGGL((sweep2_kernel<NB, NP, P_>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, \
-                       ldy, alpha, part);                                                    \
-    return;
-      DEIG_PROBE_CASE(1) DEIG_PROBE_CASE(2) DEIG_PROBE_CASE(3) DEIG_PROBE_CASE(4)
-      DEIG_PROBE_CASE(5) DEIG_PROBE_CASE(6) DEIG_PROBE_CASE(7)
-#undef DEIG_PROBE_CASE
-      default: break;
-    }
-  }
-  hipLaunchKernelGGL((sweep2_kernel<NB, NP>), grid, dim3(256), 0, st, SI, d, QS, ng, Y, ldy,
-                     alpha, part);
+  hipLaunchKernelGGL((sweep2_kernel<NB, NP, 0, PRE>), grid, dim3(256), 0, st, SI, d, QS, ng, Y,
+                     ldy, alpha, part);
 }
 
 template <int NB, int NP, bool PRE>
 void launch_v3(dim3 grid, hipStream_t st, const f32x4* SI, int64_t d, const u32x4* QS, float* Y,
                int64_t ldy, float alpha, float* part) {
-  static const int de = getenv("DEIG_SWEEP_DEPTH") ? atoi(getenv("DEIG_SWEEP_DEPTH")) : 3;
   const int64_t ng = si_groups(d);
-  if (sweep_mb(PRE, NB) == 2) {
-    if constexpr (9 * NP * NB * 1024 <= 160 * 1024) {
-      if (de == 8) {
-        hipLaunchKernelGGL((sweep3_kernel<NB, NP, 8, 1, PRE, 2>), grid, dim3(256), 0, st, SI, d,
-                           QS, ng, Y, ldy, alpha, part);
-        return;
-      }
-    }
-    if constexpr (7 * NP * NB * 1024 <= 160 * 1024) {
-      if (de == 6) {
-        hipLaunchKernelGGL((sweep3_kernel<NB, NP, 6, 1, PRE, 2>), grid, dim3(256), 0, st, SI, d,
-                           QS, ng, Y, ldy, alpha, part);
-        return;
-      }
-    }
-    if constexpr (6 * NP * NB * 1024 <= 160 * 1024) {
-      if (de == 5) {
-        hipLaunchKernelGGL((sweep3_kernel<NB, NP, 5, 1, PRE, 2>), grid, dim3(256), 0, st, SI, d,
-                           QS, ng, Y, ldy, alpha, part);
-        return;
-      }
-    }
-    if (de == 4)
-      hipLaunchKernelGGL((sweep3_kernel<NB, NP, 4, 1, PRE, 2>), grid, dim3(256), 0, st, SI, d, QS,
-                         ng, Y, ldy, alpha, part);
-    else
-      hipLaunchKernelGGL((sweep3_kernel<NB, NP, 3, 1, PRE, 2>), grid, dim3(256), 0, st, SI, d, QS,
-                         ng, Y, ldy, alpha, part);
-    return;
-  }
-  if (de == 4)
-    hipLaunchKernelGGL((sweep3_kernel<NB, NP, 4, 1, PRE>), grid, dim3(256), 0, st, SI, d, QS, ng,
-                       Y, ldy, alpha, part);
-  else if (de == 2)
-    hipLaunchKernelGGL((sweep3_kernel<NB, NP, 2, 1, PRE>), grid, dim3(256), 0, st, SI, d, QS, ng,
-                       Y, ldy, alpha, part);
+  if (sweep_mb(PRE, NB) == 2)
+    hipLaunchKernelGGL((sweep3_kernel<NB, NP, kSweepDepth, 1, PRE, 2>), grid, dim3(256), 0, st, SI,
+                       d, QS, ng, Y, ldy, alpha, part);
   else
-    hipLaunchKernelGGL((sweep3_kernel<NB, NP, 3, 1, PRE>), grid, dim3(256), 0, st, SI, d, QS, ng,
-                       Y, ldy, alpha, part);
+    hipLaunchKernelGGL((sweep3_kernel<NB, NP, kSweepDepth, 1, PRE>), grid, dim3(256), 0, st, SI, d,
+                       QS, ng, Y, ldy, alpha, part);
 }
 
 // v2 (sweep3 = false) or v3 with NP Q pieces, NB = p / 16 column blocks; PRE: the
@@ -974,7 +725,7 @@ void launch_image(bool v3, int nb, dim3 grid, hipStream_t st, const f32x4* SI, i
 #undef DEIG_NB_CASE
 }
 
-// Workspace: [Q image][split-K slabs][S image][two-piece S image] (images: v2/v3).
+// Workspace: [Q image][split-K slabs][S image][two-piece S image].
 struct SweepWs {
   u32x4* QS;
   float* part;
@@ -992,63 +743,60 @@ SweepWs sweep_carve(void* ws, int64_t d, int p) {
   const int ks = sweep_ks(d);
   if (ks > 1) off = align_up(off + (size_t)ks * d * p * sizeof(float), 256);
   w.SI = reinterpret_cast<f32x4*>(base + off);
-  if (sweep_version() != 1) off += si_bytes(d);
+  off += si_bytes(d);
   w.SH = reinterpret_cast<u32x4*>(base + off);
-  if (sweep_version() != 1) off += si_bytes(d);
+  off += si_bytes(d);
   w.total = off;
   return w;
 }
+
+// Q pieces in round_q mode (the dropped piece of Q: split_q_kernel<2>).
+constexpr int kRoundPieces = 2;
 
 }  // namespace
 
 size_t sweep_workspace_bytes(int64_t d, int p) { return sweep_carve(nullptr, d, p).total; }
 
-int sweep_prepare(const float* S, int64_t d, int64_t lds, int p, void* ws, size_t ws_bytes,
-                  hipStream_t st, const float* Vd, int64_t ldv, const float* lamd, int r) {
-  DEIG_REQUIRE(r == 0 || (Vd && lamd && ldv >= d && sweep_version() != 1),
-               "sweep: bad deflation arguments (r=%d)", r);
+int sweep_prepare(const void* S, int stype, int64_t d, int64_t lds, int p, void* ws,
+                  size_t ws_bytes, hipStream_t st, const float* Vd, int64_t ldv, const float* lamd,
+                  int r, double shift) {
+  DEIG_REQUIRE(r == 0 || (Vd && lamd && ldv >= d), "sweep: bad deflation arguments (r=%d)", r);
+  DEIG_REQUIRE(stype == DEIG_F32 || stype == DEIG_F64, "sweep: unknown element type %d", stype);
   DEIG_REQUIRE(d >= 1 && lds >= d && lds % 4 == 0 && S && aligned16(S),
                "sweep: S must be 16-byte aligned with lds >= d, lds %% 4 == 0");
   const SweepWs w = sweep_carve(ws, d, p);
   if (!ws || ws_bytes < w.total)
     return fail(DEIG_EWORKSPACE, "sweep: workspace %zu < %zu", ws_bytes, w.total);
-  if (sweep_version() == 1) return DEIG_OK;  // v1 reads S in place
   const int64_t ng = si_groups(d);
   const int64_t nunits = si_rows(d) / SI_RB * ng * 4 * 64;
-  hipLaunchKernelGGL(sweep_prepare_kernel, dim3((unsigned)cdiv(nunits, 256)), dim3(256), 0, st, S,
-                     lds, d, ng, nunits, w.SI, w.SH, Vd, ldv, lamd, r);
+  const dim3 grid((unsigned)cdiv(nunits, 256));
+  if (stype == DEIG_F64)
+    hipLaunchKernelGGL(sweep_prepare_kernel<double>, grid, dim3(256), 0, st,
+                       static_cast<const double*>(S), lds, d, ng, nunits, w.SI, w.SH, Vd, ldv,
+                       lamd, r, shift);
+  else
+    hipLaunchKernelGGL(sweep_prepare_kernel<float>, grid, dim3(256), 0, st,
+                       static_cast<const float*>(S), lds, d, ng, nunits, w.SI, w.SH, Vd, ldv,
+                       lamd, r, shift);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }
 
-// Q pieces in round_q mode: 2 unless DEIG_SWEEP_QPIECES=3 (A/B: exact Q, six
-// products, Q left untouched).
-int sweep_round_pieces() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DEIG_SWEEP_QPIECES");
-    v = (e && atoi(e) == 3) ? 3 : 2;
-  }
-  return v;
-}
-
-int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
-                float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st,
-                int mode, const SweepStep* step, bool q_ready, bool kernel_only) {
+int sweep_apply(const float* Q, int64_t d, int p, int64_t ldq, float* Y, int64_t ldy, float alpha,
+                void* ws, size_t ws_bytes, hipStream_t st, int mode, const SweepStep* step,
+                bool q_ready, bool kernel_only) {
   const bool round_q = mode >= 1;
   DEIG_REQUIRE(d >= 1 && p >= 16 && p <= 128 && p % 16 == 0,
                "sweep: need d >= 1 and p in {16, 32, ..., 128} (p=%d)", p);
-  DEIG_REQUIRE(lds >= d && lds % 4 == 0 && lds <= (1 << 24) && ldq >= p && ldy >= p,
-               "sweep: bad leading dims");
-  DEIG_REQUIRE(S && Q && Y && aligned16(S), "sweep: S must be 16-byte aligned");
+  DEIG_REQUIRE(ldq >= p && ldy >= p, "sweep: bad leading dims");
+  DEIG_REQUIRE(Q && Y, "sweep: null Q / Y");
   const SweepWs w = sweep_carve(ws, d, p);
   if (!ws || ws_bytes < w.total)
     return fail(DEIG_EWORKSPACE, "sweep: workspace %zu < %zu", ws_bytes, w.total);
   const int nb = p / 16;
   const int64_t ngrp = 2 * cdiv(d, SW_KS);
-  // v1 reads the 3-piece image only.
-  const int np = (round_q && sweep_version() != 1) ? sweep_round_pieces() : 3;
-  const bool pre = mode == 2 && np == 2 && sweep_version() != 1;
+  const int np = round_q ? kRoundPieces : 3;
+  const bool pre = mode == 2 && np == 2;
   const dim3 qgrid((unsigned)cdiv(ngrp * nb * 64, 256));
   // q_ready: the previous sweep's finish kernel already wrote this Q's image
   if (!q_ready) {
@@ -1060,41 +808,29 @@ int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, i
                          nb, ngrp, w.QS);
     DEIG_HIP_CHECK(hipGetLastError());
   }
-  const bool v3 = sweep_version() == 3 || (sweep_version() == 0 && (nb > 5 || (pre && nb >= 4)));
-  const int mbw = (sweep_version() != 1 && v3) ? sweep_mb(pre, nb) : 4;
+  // v3 (LDS-shared Q ring): above p = 80 (v2's register rings spill) and for the
+  // early-sweep mode from p = 64 (no split in the sweep, so the shared Q pays;
+  // rocprof, d = 8192: p = 80 50.6 vs 55.3 us, p = 64 47.2 vs 48.3; p = 32 at
+  // d = 3072 11.4 vs 11.0, profiles/r02l_sweep_v3pre.log; v2 stays faster with the
+  // split in the sweep)
+  const bool v3 = nb > 5 || (pre && nb >= 4);
+  const int mbw = v3 ? sweep_mb(pre, nb) : 4;
   const int ks = sweep_ks_mb(d, mbw);
-  const dim3 grid((unsigned)(cdiv(d, mbw == 4 ? SW_ROWS : 64 * mbw) * ks));
-  if (sweep_version() == 1) {
-    switch (nb) {
-      case 1: launch_v1<1>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 2: launch_v1<2>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 3: launch_v1<3>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 4: launch_v1<4>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 5: launch_v1<5>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 6: launch_v1<6>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
-      case 7: launch_v1<7>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
-      default: launch_v1<8>(grid, st, S, lds, d, w.QS, Y, ldy, alpha, w.part); break;
-    }
-  } else {
-    // v3 (above): the default above p = 80 (v2's rings spill) and for the early-sweep
-    // mode from p = 64 (no split in the sweep, so the LDS-shared Q pays; rocprof,
-    // d = 8192: p = 80 50.6 vs 55.3 us, p = 64 47.2 vs 48.3; p = 32 at d = 3072 11.4
-    // vs 11.0, profiles/r02l_sweep_v3pre.log; v2 stays faster with the split)
-    if (pre)
-      launch_image<2, true>(v3, nb, grid, st, reinterpret_cast<const f32x4*>(w.SH), d, w.QS, Y,
-                            ldy, alpha, w.part);
-    else if (np == 2)
-      launch_image<2>(v3, nb, grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part);
-    else
-      launch_image<3>(v3, nb, grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part);
-  }
+  const dim3 grid((unsigned)(cdiv(d, mbw == 4 ? SI_BR : 64 * mbw) * ks));
+  if (pre)
+    launch_image<2, true>(v3, nb, grid, st, reinterpret_cast<const f32x4*>(w.SH), d, w.QS, Y, ldy,
+                          alpha, w.part);
+  else if (np == 2)
+    launch_image<2>(v3, nb, grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part);
+  else
+    launch_image<3>(v3, nb, grid, st, w.SI, d, w.QS, Y, ldy, alpha, w.part);
   DEIG_HIP_CHECK(hipGetLastError());
   if (kernel_only) return DEIG_OK;
   if (step) {
     DEIG_REQUIRE(ldy % 4 == 0 && aligned16(Y) && step->ldq % 4 == 0 && aligned16(step->Q) &&
                      (step->kind == 1 || step->kind == 2),
                  "sweep: fused step needs 16-byte aligned Y / Q rows");
-    const int nnp = (step->next_mode >= kSweepRoundQ && sweep_version() != 1) ? sweep_round_pieces() : 3;
+    const int nnp = step->next_mode >= kSweepRoundQ ? kRoundPieces : 3;
     const float* pp = ks > 1 ? w.part : nullptr;
     const dim3 fgrid((unsigned)(4 * ngrp)), fblk((unsigned)((2 * p + 63) / 64 * 64));
     if (nnp == 2)
@@ -1116,13 +852,6 @@ int sweep_apply(const float* S, int64_t d, int64_t lds, const float* Q, int p, i
     DEIG_HIP_CHECK(hipGetLastError());
   }
   return DEIG_OK;
-}
-
-int sweep_launch(const float* S, int64_t d, int64_t lds, const float* Q, int p, int64_t ldq,
-                 float* Y, int64_t ldy, float alpha, void* ws, size_t ws_bytes, hipStream_t st) {
-  int rc = sweep_prepare(S, d, lds, p, ws, ws_bytes, st);
-  if (rc) return rc;
-  return sweep_apply(S, d, lds, Q, p, ldq, Y, ldy, alpha, ws, ws_bytes, st, 0);
 }
 
 }  // namespace deig

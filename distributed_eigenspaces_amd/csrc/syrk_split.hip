@@ -564,6 +564,190 @@ __device__ __forceinline__ void segment(const SSched& s, unsigned char* lds, int
   }
 }
 
+// ------------------------------------------------ staggered phases (variants 172 / 174)
+// The K-tile's work split into P phases, each an L part (this phase's ds_reads of
+// the A fragments - and the B fragments in phase 0 - plus some of the next
+// K-tile's LDS-DMA pieces) and an M part (its 96 / P MFMAs), each part closed by
+// a raw s_barrier; waves 4-7 run ONE BARRIER BEHIND waves 0-3.  Waves w and w + 4
+// share a SIMD, so between any two barriers one of them issues MFMAs while its
+// partner issues loads: the SIMD's matrix pipe stays fed instead of idling while
+// both waves issue their DMA pieces right after a common barrier (the lockstep K
+// loop above: MFMA busy 0.71, profiles/r02p_pmc_sq_tcc_syrk_c3.txt).  Same
+// 2-stage ring, same MFMA order per accumulator (bit-identical sums).
+//   RAW: the next K-tile's pieces go out in phases q < QD of this one and each wave
+//   waits for its own (vmcnt(0)) at the end of L_{P-1}, before the barrier that
+//   precedes the first read of that buffer by either group.
+//   WAR: every L part retires its reads (lgkmcnt(0)) before its closing barrier, and
+//   a buffer is restaged from the next K-tile's L_0 on - after the lagging group's
+//   last read of it (its L_{P-1} of the K-tile before) has passed that barrier.
+template <int P>
+__device__ __forceinline__ void segment_st(const SSched& s, unsigned char* lds, int tile,
+                                           int64_t k0, int64_t k1, int slot, bool partial,
+                                           int pace_j) {
+  static_assert(P == 2 || P == 4, "phases per K-tile");
+  constexpr int MBP = 8 / P;              // A blocks (16 rows) per phase
+  constexpr int QD = P == 2 ? 1 : 2;      // phases that issue the next K-tile's pieces
+  constexpr int BUF_B = Geo<2>::BUF_B;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wi = wave >> 2, wj = wave & 3;
+  const bool lag = wave >= 4;  // the group one barrier behind
+  const int lane16 = lane * 16;
+  const int tt = __builtin_amdgcn_readfirstlane(s.order[tile]);
+  const int ti = tt & 0xffff, tj = tt >> 16;
+  const int i0 = ti * BT, j0 = tj * BT;
+  const bool diag = (ti == tj);
+  Acc<16> acc;
+  acc.zero();
+  float* slab = partial ? s.part + (int64_t)slot * SLAB : s.accs + (int64_t)blockIdx.x * SLAB;
+  bool flushed = false;
+  const int64_t nkt = k1 - k0;
+  auto bar = [&]() {  // raw barrier; nothing moves across it
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+  };
+  // this wave's LDS-DMA pieces [u0, u1) of K-tile kt into buf (8 off the diagonal:
+  // slices wave*2 .. +1 of [A | B] x four 1-KiB parts; 4 on it: panel A only)
+  auto stage_part = [&](int64_t kt, unsigned char* buf, int u0, int u1) {
+    const int64_t blk = kt;  // KT = 2: one 32-row block per K-tile
+    const i32x4 rsrc = make_rsrc(s.XP + blk * (int64_t)s.nt * BLOCK_B, (uint32_t)(s.nt * BLOCK_B));
+    int l16 = lane16;
+    asm volatile("" : "+v"(l16));
+    if (!diag) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (i < u0 || i >= u1) continue;
+        const int c = wave * 2 + (i >> 2), p = i & 3;
+        const int pb = c / 8, sl = c % 8;
+        const int g = (pb ? j0 : i0) / BT * BLOCK_B + sl * SLICE_B;
+        dma16(rsrc, l16 + g + p * 1024, buf + pb * Geo<2>::PANEL_B + sl * SLICE_B + p * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i < u0 / 2 || i >= u1 / 2) continue;
+        const int idx = wave * 4 + i;
+        const int sl = idx >> 2, p = idx & 3;
+        dma16(rsrc, l16 + i0 / BT * BLOCK_B + sl * SLICE_B + p * 1024, buf + sl * SLICE_B + p * 1024);
+      }
+    }
+  };
+  if (nkt > 0) {
+    wait_vm<0>();     // the previous segment's stores / flushes
+    __syncthreads();  // ... and its last reads of the ring
+    stage_part(k0, lds, 0, 8);
+    wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    if (lag) bar();  // the stagger
+    const int c = lane & 15, g4 = lane >> 4;
+    int since = 0, since_pace = 0;
+    const int xcd = blockIdx.x & 7;
+    const unsigned nx = (unsigned)((s.G >> 3) + (xcd < (s.G & 7) ? 1 : 0));
+    bf16x8 bhi[4], blo[4];
+    for (int64_t t = 0; t < nkt; ++t) {
+      const unsigned char* cur = lds + (t & 1) * BUF_B;
+      unsigned char* nxt = lds + ((t + 1) & 1) * BUF_B;
+      const bool more = t + 1 < nkt;
+      const unsigned char* ph = cur + ((g4 * 2) * BT + 128 * wi + c) * 16;
+      const unsigned char* qh = (diag ? cur : cur + Geo<2>::PANEL_B) + ((g4 * 2) * BT + 64 * wj + c) * 16;
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        // ---------------- L part
+        if (q == 0) {
+          if (pace_j >= 0 && ++since_pace == s.pace_kt) {
+            since_pace = 0;
+            ++pace_j;
+            if (threadIdx.x == 0) xcd_pace(s.pace + 32 * xcd, (unsigned)pace_j * nx);
+          }
+          if (since == s.flush_kt) {  // no DMA in flight here (waited in L_{P-1})
+            flush<16>(slab, !flushed, acc, wave, lane);
+            wait_vm<0>();
+            flushed = true;
+            since = 0;
+          }
+          ++since;
+        }
+        if (more && q < QD) stage_part(k0 + t + 1, nxt, q * (8 / QD), (q + 1) * (8 / QD));
+        if (q == 0) {
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb) {
+            bhi[nb] = *reinterpret_cast<const bf16x8*>(qh + (16 * nb) * 16);
+            blo[nb] = *reinterpret_cast<const bf16x8*>(qh + (BT + 16 * nb) * 16);
+          }
+        }
+        bf16x8 ahi[MBP], alo[MBP];
+#pragma unroll
+        for (int m = 0; m < MBP; ++m) {
+          const int mb = q * MBP + m;
+          ahi[m] = *reinterpret_cast<const bf16x8*>(ph + (16 * mb) * 16);
+          alo[m] = *reinterpret_cast<const bf16x8*>(ph + (BT + 16 * mb) * 16);
+        }
+        if (more && q == P - 1) wait_vm<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        bar();
+        // ---------------- M part
+#pragma unroll
+        for (int m = 0; m < MBP; ++m) {
+          const int mb = q * MBP + m;
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb)
+            acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[m], bhi[nb], acc.a[mb][nb], 0, 0, 0);
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb)
+            acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[m], blo[nb], acc.a[mb][nb], 0, 0, 0);
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb)
+            acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[m], bhi[nb], acc.a[mb][nb], 0, 0, 0);
+        }
+        bar();
+      }
+    }
+    if (!lag) bar();  // balance the stagger
+  }
+  if (flushed) unflush<16>(slab, acc, wave, lane);
+  if (partial) {
+#pragma unroll
+    for (int q = 0; q < NQUAD; ++q)
+      *slab_at(slab, wave, q, lane) = f32x4{acc.at(q, 0), acc.at(q, 1), acc.at(q, 2), acc.at(q, 3)};
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < NQUAD; ++q) {
+    const float a[4] = {acc.at(q, 0), acc.at(q, 1), acc.at(q, 2), acc.at(q, 3)};
+    store4(s, i0 + 128 * wi + Acc<16>::qrow(q, lane), j0 + 64 * wj + Acc<16>::qcol(q, lane), diag, a);
+  }
+}
+
+template <int P>
+__global__ __launch_bounds__(NTHR) void syrks_st_kernel(SSched s) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * Geo<2>::BUF_B];
+  const int L = xcd_logical(blockIdx.x, s.G);
+  // work decomposition as syrks_kernel (full phases, then K-synchronous remainder
+  // segments)
+  const int items = s.R * s.nseg;
+  const int nwork = s.q + (L < items ? (items - 1 - L) / s.G + 1 : 0);
+  for (int w = 0; w < nwork; ++w) {
+    int tile, slot = 0;
+    int64_t k0 = 0, k1 = s.NK;
+    const bool partial = w >= s.q;
+    if (!partial) {
+      tile = w * s.G + L;
+    } else {
+      const int i = L + (w - s.q) * s.G;
+      const int sg = i / s.R, r = i - sg * s.R;
+      tile = s.q * s.G + r;
+      slot = i;
+      k0 = __builtin_amdgcn_readfirstlane((int)(s.NK * sg / s.nseg));
+      k1 = __builtin_amdgcn_readfirstlane((int)(s.NK * (sg + 1) / s.nseg));
+    }
+    const int pace_j = (!partial && s.pace_kt > 0) ? (int)(w * (s.NK / s.pace_kt)) : -1;
+    segment_st<P>(s, lds, tile, k0, k1, slot, partial, pace_j);
+  }
+}
+
 template <int MF, int KT, int NST, bool FX>
 __global__ __launch_bounds__(NTHR) void syrks_kernel(SSched s) {
   static_assert(NST * Geo<KT>::BUF_B <= 160 * 1024, "LDS ring exceeds 160 KiB");
@@ -713,10 +897,6 @@ __global__ void tile_order_kernel(int nt, int* order) {
 // ceil(R nseg / G) / nseg (in full-tile passes) is within 2 % of the best.
 int remainder_segments(int64_t R, int G) {
   if (R <= 0) return 0;
-  if (const char* v = getenv("DEIG_SYRK_SEGS")) {
-    const int e = atoi(v);
-    if (e >= 1 && e <= 256) return e;
-  }
   double best = 1e30;
   for (int k = 1; k <= 64; ++k) best = fmin(best, (double)cdiv(R * k, G) / k);
   for (int k = 1; k <= 64; ++k)
@@ -775,10 +955,14 @@ int64_t default_chunk_rows(int64_t n, int64_t d) {
 // 1/d while the fused split's stays.  Measured (r02, interleaved A/B in one
 // process, profiles/r02l_syrk_fused_ab.log): d = 3072 (config 2) fused 27.3 ms vs
 // 29.0 ms; d = 8192 (config 3 shard) fused 370 ms vs 336 ms.
-// DEIG_SYRK_VARIANT selects one for A/B measurements.
+// A/B builds (tools/, never the shipped library) fix one with -DDEIG_AB_SYRK_VARIANT=N.
 int syrk_variant(int64_t d) {
-  if (const char* v = getenv("DEIG_SYRK_VARIANT")) return atoi(v);
+#ifdef DEIG_AB_SYRK_VARIANT
+  (void)d;
+  return DEIG_AB_SYRK_VARIANT;
+#else
   return d <= 4096 ? 163 : 162;
+#endif
 }
 
 }  // namespace
@@ -836,21 +1020,18 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
   // (config 3, n = 2^21: 8192 - vs 4096 the op ran 337.6 -> 331.1 ms with sampled
   // error 5.0e-7 -> 4.7e-7, profiles/r02l_syrk_flush.log; fewer flushes, each a
   // read-add-write of the block's 256 KiB slab beside stalled MFMAs).
-  // DEIG_SYRK_FLUSH_ROWS overrides, for A/B runs.
   int64_t flush_rows = 4096;
   while (flush_rows < 16384 && (flush_rows * 2) * (flush_rows * 2) <= 32 * n) flush_rows *= 2;
-  if (const char* v = getenv("DEIG_SYRK_FLUSH_ROWS")) flush_rows = atoll(v);
-  if (flush_rows < 32) flush_rows = 32;
-  if (flush_rows > (int64_t(1) << 30)) flush_rows = int64_t(1) << 30;
-  s.prio = 0;
-  if (const char* v = getenv("DEIG_SYRK_PRIO")) s.prio = atoi(v);
+  s.prio = 0;  // s_setprio staggering measured slower (374 vs 342 ms, r02)
   s.pace = reinterpret_cast<unsigned*>(base + L.off_pace);
   // XCD pacing every 64 K-tiles (2048 rows): config 3 L2 hit rate 0.52 -> 0.75, fabric
   // read requests halved, 345 -> 334 ms (r02, interleaved A/B in one process;
-  // 16 / 32 / 128 / 256 K-tiles measured 0.3-1.5 % slower).  DEIG_SYRK_PACE=0: off.
+  // 16 / 32 / 128 / 256 K-tiles measured 0.3-1.5 % slower).
+#ifdef DEIG_AB_SYRK_PACE
+  s.pace_kt = DEIG_AB_SYRK_PACE;
+#else
   s.pace_kt = 64;
-  if (const char* v = getenv("DEIG_SYRK_PACE")) s.pace_kt = atoi(v);
-  if (s.pace_kt < 0) s.pace_kt = 0;
+#endif
   hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(64), 0, stream, s.nt,
                      reinterpret_cast<int*>(base + L.off_order));
   DEIG_HIP_CHECK(hipGetLastError());
@@ -859,10 +1040,12 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
   s.nrows = n;
   s.corr = corr;
   if (fused) {
-    DEIG_REQUIRE(ldx <= (int64_t(1) << 25), "syrk: ldx > 2^25 needs DEIG_SYRK_VARIANT=162");
+    DEIG_REQUIRE(ldx <= (int64_t(1) << 25), "syrk: ldx > 2^25 is not supported for d <= 4096");
     // One pass over all n rows (no XP image, no chunks).  lo^2 partials:
     // [segment < max(1, nseg)][octet wave < 4][dp], zero where no diagonal tile wrote.
     const int64_t yb = 4 * (L.nseg > 1 ? L.nseg : 1);
+    DEIG_REQUIRE(yb <= L.yb_max, "syrk: %lld lo^2 partial rows exceed the workspace's %lld",
+                 (long long)yb, (long long)L.yb_max);
     DEIG_HIP_CHECK(hipMemsetAsync(corr, 0, sizeof(float) * (size_t)(yb * L.dp), stream));
     s.NK = cdiv(n, ROWS_PAD);
     s.nseg = (int)L.nseg;
@@ -899,6 +1082,8 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
     const bool mf16 = variant >= 100;
     if (s.pace_kt > 0) DEIG_HIP_CHECK(hipMemsetAsync(s.pace, 0, 8 * 128, stream));
     switch (variant) {
+      case 172: hipLaunchKernelGGL(syrks_st_kernel<2>, dim3(G), dim3(NTHR), 0, stream, s); break;
+      case 174: hipLaunchKernelGGL(syrks_st_kernel<4>, dim3(G), dim3(NTHR), 0, stream, s); break;
       case 13: hipLaunchKernelGGL((syrks_kernel<32, 1, 3, false>), dim3(G), dim3(NTHR), 0, stream, s); break;
       case 14: hipLaunchKernelGGL((syrks_kernel<32, 1, 4, false>), dim3(G), dim3(NTHR), 0, stream, s); break;
       case 15: hipLaunchKernelGGL((syrks_kernel<32, 1, 5, false>), dim3(G), dim3(NTHR), 0, stream, s); break;

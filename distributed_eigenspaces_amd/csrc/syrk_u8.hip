@@ -5,8 +5,9 @@
 //                  the reference's grayscale + flatten, distributed.py:170-173
 //                  (data.mean(axis=3), reshape to 1024) followed by :59-70.
 // The reference computes in float64 from the uint8 CIFAR bytes (load_data.py:18-33);
-// here every product and sum is EXACT (integers), so S is the correctly rounded
-// fp32 (or fp64) value of the reference's result - no accumulation error at all,
+// here every product and sum is EXACT (integers), so S is the exact result rounded
+// once (fp64; fp32 within 1 ulp of the correctly rounded value, u8_finalize_kernel)
+// - no accumulation error at all,
 // which an fp32 SYRK of uncentered 0..255 data cannot offer (its rounding noise
 // ~5e-7 max|S| alone moves a CIFAR-like top-k basis by ~3e-4 in ||P - P_ref||_F).
 //
@@ -245,12 +246,17 @@ __global__ __launch_bounds__(SYRK_THR) void u8_syrk_kernel(U8Sched s) {
 }
 
 // One thread per S entry: the lower-triangle value of (max(i,j), min(i,j)) from
-// the exact int64 sums, scaled once in double, stored to both triangles.
+// the exact int64 sums, scaled in double, stored to both triangles.  div > 0 (alpha
+// == 1/n, the reference's /= n): v = a / (div * 9 for gray), ONE rounding of the
+// exact quotient (div * 9 is exact); else alpha * a (/ 9).  The fp32 S is that
+// double rounded to float: the correctly rounded value except in the ~2^-29 of
+// cases where the double lands on a float tie (then 1 ulp).
 template <int MODE>
 __global__ __launch_bounds__(256) void u8_finalize_kernel(const unsigned long long* __restrict__ G,
                                                           const unsigned long long* __restrict__ colsum,
                                                           int64_t fpad, int64_t d, int64_t n,
-                                                          double alpha, float* __restrict__ S,
+                                                          double alpha, int64_t div,
+                                                          float* __restrict__ S,
                                                           int64_t lds, double* __restrict__ S64,
                                                           int64_t lds64) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -262,14 +268,14 @@ __global__ __launch_bounds__(256) void u8_finalize_kernel(const unsigned long lo
   double v;
   if (MODE == DEIG_U8_RAW) {
     a = (long long)G[i * fpad + j] + 128ll * (ci + cj) + 16384ll * n;
-    v = alpha * (double)a;
+    v = div > 0 ? (double)a / (double)div : alpha * (double)a;
   } else {
     const int64_t pl = fpad * fpad;
     const long long phh = (long long)G[i * fpad + j];
     const long long pll = (long long)G[pl + i * fpad + j];
     const long long pww = (long long)G[2 * pl + i * fpad + j];
     a = 240ll * phh + 16ll * pww - 15ll * pll + 384ll * (ci + cj) + 147456ll * n;
-    v = alpha * (double)a / 9.0;
+    v = div > 0 ? (double)a / (9.0 * (double)div) : alpha * (double)a / 9.0;
   }
   if (S) S[r * lds + c] = (float)v;
   if (S64) S64[r * lds64 + c] = v;
@@ -371,12 +377,13 @@ int syrk_u8_launch(const uint8_t* X, int64_t n, int64_t d, int64_t ldx, int mode
                      dim3(SYRK_THR), 0, stream, s);
   DEIG_HIP_CHECK(hipGetLastError());
   const dim3 fg((unsigned)cdiv(d * d, 256));
+  const int64_t div = (alpha == 1.0 / (double)n && n < (int64_t(1) << 48)) ? n : 0;
   if (mode == DEIG_U8_RAW)
     hipLaunchKernelGGL(u8_finalize_kernel<DEIG_U8_RAW>, fg, dim3(256), 0, stream, G, col, L.fpad, d,
-                       n, alpha, S, lds, S64, lds64);
+                       n, alpha, div, S, lds, S64, lds64);
   else
     hipLaunchKernelGGL(u8_finalize_kernel<DEIG_U8_GRAY3>, fg, dim3(256), 0, stream, G, col, L.fpad,
-                       d, n, alpha, S, lds, S64, lds64);
+                       d, n, alpha, div, S, lds, S64, lds64);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }

@@ -3,7 +3,8 @@
 Same classes, methods, arguments, message schema and CLI flags; the arithmetic
 runs on the GPU through the HIP hot path:
 
-* ``SlaveNode.compute_sigma_hat_``  (distributed.py:59-70)  -> fp32-MFMA SYRK
+* ``SlaveNode.compute_sigma_hat_``  (distributed.py:59-70)  -> MFMA SYRK (float64 data:
+  mean-shifted, float64 result; uint8: exact integer)
 * ``Node.top_k_eigenvectors``       (distributed.py:22-29)  -> subspace iteration + RR
 * ``MasterNode.callback_`` average  (distributed.py:126-130) -> implicit projector-average
   top-k (the reference builds the d x d sigma_tilde and discards it; the notebook's
@@ -30,9 +31,11 @@ reference accepts):
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import threading
 import time
+import weakref
 from contextlib import nullcontext
 
 import numpy as np
@@ -55,30 +58,67 @@ _dev_cache: dict = {}
 _dev_lock = threading.Lock()
 
 
+def _fingerprint(a: np.ndarray):
+    """Cheap content check of a host array: shape, dtype and a hash of up to 64K
+    evenly spaced elements (catches ``data[:] = new`` on a reused buffer)."""
+    flat = a.reshape(-1)
+    step = max(1, flat.size // 65536)
+    return (a.shape, a.dtype.str, hashlib.blake2b(np.ascontiguousarray(flat[::step]).tobytes(),
+                                                  digest_size=16).digest())
+
+
+def _drop(key):
+    with _dev_lock:
+        _dev_cache.pop(key, None)
+
+
+def clear_device_cache():
+    """Forget every cached device copy of node data (see ``_device_copy``)."""
+    with _dev_lock:
+        _dev_cache.clear()
+
+
 def _device_copy(data) -> torch.Tensor:
     """The node's data on the GPU, shared by every node given the same host array
     (threaded workers hold one device copy).  uint8 samples stay uint8 (the exact
-    integer covariance path); everything else becomes float32."""
-    if isinstance(data, torch.Tensor) and data.is_cuda and data.dtype in (torch.uint8, torch.float32):
+    integer covariance path), float64 stays float64 (the reference's dtype: the
+    mean-shifted covariance path), everything else becomes float32.
+
+    The cache holds the device copy only while the host array is alive (weak
+    reference; the entry is dropped when the array is freed) and re-uploads when a
+    sampled fingerprint of the array's contents changed.  ``clear_device_cache()``
+    forgets everything."""
+    if isinstance(data, torch.Tensor) and data.is_cuda and \
+            data.dtype in (torch.uint8, torch.float32, torch.float64):
         return data
+    if not torch.cuda.is_available():
+        raise RuntimeError("SlaveNode: needs a ROCm GPU; there is no CPU fallback")
+    arr = data if isinstance(data, np.ndarray) else None
+    key = id(data)
+    fp = _fingerprint(arr) if arr is not None else None
     with _dev_lock:
-        hit = _dev_cache.get(id(data))
-        if hit is not None and hit[0] is data:
-            return hit[1]
-        t = torch.as_tensor(data)
-        if t.dtype == torch.uint8:
-            if not torch.cuda.is_available():
-                raise RuntimeError("SlaveNode: needs a ROCm GPU; there is no CPU fallback")
-            dev = t.to(torch.device("cuda", torch.cuda.current_device()))
-        else:
-            dev = linalg.require_device_tensor(t, "SlaveNode.data")
-        _dev_cache[id(data)] = (data, dev)
-        return dev
+        hit = _dev_cache.get(key)
+        if hit is not None and hit[0]() is data and hit[1] == fp:
+            return hit[2]
+    t = torch.as_tensor(data)
+    if t.dtype == torch.uint8:
+        dev = t.to(torch.device("cuda", torch.cuda.current_device()))
+    else:
+        dev = linalg.require_device_tensor(t, "SlaveNode.data", keep_f64=True)
+    if arr is not None:
+        try:
+            ref = weakref.ref(arr, lambda _r, k=key: _drop(k))
+        except TypeError:  # not weak-referenceable: no caching
+            return dev
+        with _dev_lock:
+            _dev_cache[key] = (ref, fp, dev)
+    return dev
 
 
 def top_k_eigh(matrix, k: int):
-    """(eigenvalues ascending, eigenvectors d x k ascending) of a symmetric matrix."""
-    res = linalg.topk_eigh(matrix, int(k))
+    """(eigenvalues ascending, eigenvectors d x k ascending) of a symmetric matrix
+    (any symmetric input, any 1 <= k <= d, like distributed.py:29's eigh)."""
+    res = linalg.topk_eigh(linalg.require_device_tensor(matrix, "matrix", keep_f64=True), int(k))
     if _is_numpy(matrix):
         w = res.evals.double().cpu().numpy()
         v = np.asfortranarray(res.V.double().cpu().numpy())
@@ -92,11 +132,20 @@ def top_k_eigenvectors(matrix, k: int):
 
 
 def compute_sigma_hat(x):
-    """``SlaveNode.compute_sigma_hat_`` (distributed.py:59-70): X^T X / n, uncentered."""
-    S = linalg.sigma_hat(x)
+    """``SlaveNode.compute_sigma_hat_`` (distributed.py:59-70): X^T X / n, uncentered.
+
+    numpy in -> float64 numpy out, like the reference: float samples take the
+    mean-shifted path (float64 result), uint8 samples the exact integer path
+    (float64 result).  GPU tensors: float32 -> the float32 SYRK, float64 -> the
+    shifted path (float64), uint8 -> exact (float64)."""
     if _is_numpy(x):
-        return S.double().cpu().numpy()
-    return S
+        a = np.asarray(x)
+        t = torch.as_tensor(a if a.dtype in (np.uint8, np.float64) else a.astype(np.float64))
+        S = linalg.sigma_hat(t, dtype=torch.float64)
+        return S.cpu().numpy()
+    if x.dtype == torch.uint8:
+        return linalg.sigma_hat(x, dtype=torch.float64)
+    return linalg.sigma_hat(x)
 
 
 class Node:
@@ -273,6 +322,19 @@ def load_dataset(path):
     return data
 
 
+def cli_broker(broker: str, mode):
+    """The broker a CLI node connects to.  ``--mode slave`` / ``--mode master`` are
+    separate processes, as in the reference, whose ``--broker`` is a RabbitMQ host
+    name (``pika.ConnectionParameters(host)``, distributed.py:16): a bare host or IP
+    there means the socket broker on that host at pika's default port 5672 (start
+    it with ``python -m distributed_eigenspaces_amd.broker --serve HOST:5672``).  An
+    in-process broker name cannot connect two processes, so it is never chosen for
+    those modes; ``--mode local`` keeps in-process names."""
+    if mode in ("slave", "master") and _broker.parse_address(broker) is None:
+        return f"tcp://{broker}:5672"
+    return broker
+
+
 def main(argv=None):
     parser = argparse.ArgumentParser(description="Multinode PCA")
     parser.add_argument("--mode", help="Mode to run script - slave, master or local")
@@ -285,11 +347,12 @@ def main(argv=None):
     args = parser.parse_args(argv)
     if args.broker is None:
         raise RuntimeError("Broker not specified")
+    broker = cli_broker(args.broker, args.mode)
     data = load_dataset(args.data)
     if args.mode == "slave":
-        return run_slave(args.broker, data)
+        return run_slave(broker, data)
     elif args.mode == "master":
-        return run_master(args.broker, int(args.rank), int(args.batches), data)
+        return run_master(broker, int(args.rank), int(args.batches), data)
     elif args.mode == "local":
         return run_local(int(args.rank), int(args.batches), data, args.broker)
     raise RuntimeError("Mode not specified or specified wrong")

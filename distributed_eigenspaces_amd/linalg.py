@@ -23,12 +23,13 @@ from . import _lib
 __all__ = [
     "sigma_hat", "topk_eigh", "projavg_topk", "oja_step", "default_subspace",
     "EigResult", "require_device_tensor", "project", "stack_bases", "gemm_skinny",
-    "oja_steps", "sym_apply", "sym_power", "sigma_hat_u8",
+    "oja_steps", "sym_apply", "sym_power", "sigma_hat_u8", "sigma_hat_shift",
 ]
 
 DEFAULT_TOL = 1e-6
 DEFAULT_MAX_SWEEPS = 300
-MAX_K = 128  # the solvers' subspace cap (kMaxP in csrc/capi.hip)
+MAX_P = 128  # widest subspace of one solver block (kMaxP in csrc/capi.hip); k > 128
+             # is solved in locked blocks of p - 16 pairs
 
 
 class IndefiniteWarning(RuntimeWarning):
@@ -69,8 +70,10 @@ def _stream(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
-def require_device_tensor(t, name: str = "input") -> torch.Tensor:
-    """float32 tensor on a ROCm device (host arrays are copied over).  No CPU path."""
+def require_device_tensor(t, name: str = "input", keep_f64: bool = False) -> torch.Tensor:
+    """float32 tensor on a ROCm device (host arrays are copied over).  No CPU path.
+    keep_f64: float64 input stays float64 (the reference's dtype; the covariance and
+    the solver take it as is)."""
     if not torch.cuda.is_available():
         raise RuntimeError(
             f"{name}: distributed_eigenspaces_amd runs only on a ROCm GPU (MI355X); "
@@ -79,6 +82,8 @@ def require_device_tensor(t, name: str = "input") -> torch.Tensor:
         t = torch.as_tensor(t)
     if t.device.type != "cuda":
         t = t.to(device=torch.device("cuda", torch.cuda.current_device()))
+    if keep_f64 and t.dtype == torch.float64:
+        return t
     if t.dtype != torch.float32:
         t = t.to(torch.float32)
     return t
@@ -105,22 +110,32 @@ def default_subspace(d: int, k: int) -> int:
 
 # ---------------------------------------------------------------- covariance
 def sigma_hat(x: torch.Tensor, alpha: float | None = None,
-              out: torch.Tensor | None = None, algo: str = "auto") -> torch.Tensor:
+              out: torch.Tensor | None = None, algo: str = "auto",
+              shift: bool | None = None, dtype: torch.dtype | None = None) -> torch.Tensor:
     """Sigma_hat = alpha * X^T X with alpha = 1/n by default (uncentered).
 
     GPU replacement for ``SlaveNode.compute_sigma_hat_`` (distributed.py:59-70).
-    x: (n, d) float32 on the GPU.  Returns a (d, d) float32 tensor, bit-exactly
-    symmetric.  Columns are zero-padded to a multiple of 4 internally if needed.
-    algo: "split3" (fp32 operands as bf16 hi/lo pairs on bf16 MFMA, fp32
-    accumulation, see include/deig.h), "fp32" (f32 MFMA fma chain) or "auto"
-    (default: split3 for n >= 1024 rows, fp32 below).
+    x: (n, d) on the GPU (host arrays are copied over):
+      * float32 (default path): a (d, d) float32 tensor, bit-exactly symmetric.
+        algo: "split3" (fp32 operands as bf16 hi/lo pairs on bf16 MFMA, fp32
+        accumulation, see include/deig.h), "fp32" (f32 MFMA fma chain) or "auto"
+        (split3 for n >= 1024 rows, fp32 below);
+      * float64 (the reference's dtype, distributed.py:171) or ``shift=True``: the
+        mean-shifted covariance (deig_syrk_shift: the SYRK runs on X - mu, the mean
+        terms are added in double) returned as float64 - the small eigenvectors of an
+        uncentered covariance keep float64 parity (csrc/shift.hip);
+      * uint8 samples: the exact integer path (sigma_hat_u8; 2-D raw bytes or
+        N x H x W x 3 pixels with the reference's grayscale fused in).
+    dtype: result dtype (float32 / float64) for the shifted and uint8 paths.
     """
     if not isinstance(x, torch.Tensor):
         x = torch.as_tensor(x)
     if x.dtype == torch.uint8:
-        # uint8 samples: the exact integer path (2-D raw bytes, or N x H x W x 3
-        # pixels with the reference's grayscale fused in)
-        return sigma_hat_u8(x, alpha=alpha, out=out)
+        return sigma_hat_u8(x, alpha=alpha, out=out, dtype=dtype or torch.float32)
+    if shift is None:
+        shift = x.dtype == torch.float64
+    if shift:
+        return sigma_hat_shift(x, alpha=alpha, out=out, dtype=dtype or torch.float64)
     if algo not in _lib.SYRK_ALGOS:
         raise ValueError(f"algo must be one of {sorted(_lib.SYRK_ALGOS)}, got {algo!r}")
     code = _lib.SYRK_ALGOS[algo]
@@ -153,6 +168,47 @@ def sigma_hat(x: torch.Tensor, alpha: float | None = None,
         if out is not None:
             out.copy_(S)
             return out
+    return S
+
+
+def sigma_hat_shift(x: torch.Tensor, alpha: float | None = None,
+                    out: torch.Tensor | None = None,
+                    dtype: torch.dtype = torch.float64) -> torch.Tensor:
+    """Mean-shifted covariance alpha * X^T X (alpha = 1/n: distributed.py:59-70) of
+    float32 / float64 samples (include/deig.h deig_syrk_shift): the SYRK runs on
+    C = fl32(X - mu) and the mean terms are added in double, so its rounding is
+    relative to the centred data instead of the dominant mean direction of an
+    uncentered covariance.  Returns a (d, d) tensor of ``dtype`` (float64: the
+    reference's), bit-exactly symmetric."""
+    if not isinstance(x, torch.Tensor):
+        x = torch.as_tensor(x)
+    if x.dtype not in (torch.float32, torch.float64):
+        x = x.to(torch.float64)
+    x = require_device_tensor(x, "sigma_hat_shift", keep_f64=True)
+    if x.dim() != 2:
+        raise ValueError(f"x must be 2-D (n, d), got {tuple(x.shape)}")
+    if dtype not in (torch.float32, torch.float64):
+        raise ValueError("dtype must be torch.float32 or torch.float64")
+    n, d = x.shape
+    if n == 0:
+        return torch.full((d, d), float("nan"), dtype=dtype, device=x.device)
+    if x.stride(1) != 1 or x.stride(0) < d:
+        x = x.contiguous()
+    a = (1.0 / n) if alpha is None else float(alpha)
+    xtype = _lib.DEIG_F64 if x.dtype == torch.float64 else _lib.DEIG_F32
+    S = torch.empty((d, d), dtype=dtype, device=x.device)
+    f64 = dtype == torch.float64
+    L = _lib.lib()
+    with torch.cuda.device(x.device):
+        nbytes = L.deig_syrk_shift_workspace(n, d, xtype)
+        ws = _workspace(x.device, nbytes)
+        rc = L.deig_syrk_shift(x.data_ptr(), xtype, n, d, x.stride(0), ctypes.c_double(a),
+                               S.data_ptr() if f64 else None, d, None if f64 else S.data_ptr(), d,
+                               ws.data_ptr(), nbytes, _stream(x.device))
+    _lib.check(rc, "deig_syrk_shift")
+    if out is not None:
+        out.copy_(S)
+        return out
     return S
 
 
@@ -258,41 +314,38 @@ def _warm(q0, d, device):
 
 def topk_eigh(S: torch.Tensor, k: int, *, p: int | None = None, tol: float = DEFAULT_TOL,
               max_sweeps: int = DEFAULT_MAX_SWEEPS, q0: torch.Tensor | None = None,
-              check_finite: bool = True) -> EigResult:
+              check_finite: bool = True, opts: "_lib.SolverOpts | None" = None) -> EigResult:
     """Top-k eigenpairs of a symmetric matrix, ascending (GPU subspace iteration).
 
     GPU replacement for ``Node.top_k_eigenvectors`` (distributed.py:22-29:
     ``eigh(matrix, eigvals=(N-k, N-1))[1]``) that also returns the eigenvalues.
+    Like scipy's ``?syevr`` call it takes any symmetric S and any 1 <= k <= d
+    (ValueError outside, like scipy's subset_by_index check): k > 128 runs in
+    locked blocks of p - 16 pairs, and an indefinite S is detected from the Ritz
+    values and solved as S + sigma I (include/deig.h deig_topk_sym_ex).  A float64
+    S (the reference's dtype) is read in double by the image and deflation passes.
     Only the lower triangle matters mathematically, but the full matrix is read
-    (the SYRK output is bit-exactly symmetric).  Raises ValueError for k outside
-    [1, d] like scipy's subset_by_index check, and for k > 128 (the subspace cap).
-
-    S must be symmetric positive semi-definite, as the reference's inputs are
-    (covariances, projector averages, their online sums): subspace iteration
-    finds the largest-magnitude eigenvalues and the Chebyshev filter damps [0, c],
-    so on an indefinite S with |lambda_min| > lambda_k the result can differ from
-    eigh's; a NotConvergedWarning-style ``IndefiniteWarning`` flags a returned
-    eigenvalue below -1e-6 |lambda_max|.  Zero padding (d % 4 != 0, or a subspace
-    wider than d when k is close to d) adds zero eigenvalues: for a rank-deficient
-    S whose top-k reaches into its null space those k-th vectors are arbitrary
-    null-space vectors, as with eigh, but may lie partly in the padding.
+    (the SYRK output is bit-exactly symmetric).  Zero padding (d % 4 != 0, or a
+    subspace wider than d when k is close to d) adds zero eigenvalues: for a
+    rank-deficient S whose top-k reaches into its null space those k-th vectors
+    are arbitrary null-space vectors, as with eigh, but may lie partly in the
+    padding.  ``opts``: solver options (``_lib.solver_opts(...)``).
     """
-    S = require_device_tensor(S, "topk_eigh")
+    S = require_device_tensor(S, "topk_eigh", keep_f64=True)
     if S.dim() != 2 or S.shape[0] != S.shape[1]:
         raise ValueError(f"expected a square matrix, got {tuple(S.shape)}")
     d = S.shape[0]
     k = int(k)
     if not 1 <= k <= d:
         raise ValueError(f"k={k} out of range [1, {d}]")
-    if k > MAX_K:
-        raise ValueError(f"k={k} > {MAX_K}: the GPU solver's subspace is capped at {MAX_K} columns")
     if check_finite and not bool(torch.isfinite(S).all()):
         raise ValueError("array must not contain infs or NaNs")
     dp = _pad_dim(d)
     if not p:  # a subspace wider than d (k close to a small d): pad d up to it
-        dp = max(dp, default_subspace(max(dp, (k + 15) // 16 * 16), k))
-    if dp != d or S.stride(1) != 1 or S.stride(0) % 4 or S.data_ptr() % 16:
-        Sp = torch.zeros((dp, dp), dtype=torch.float32, device=S.device)
+        dp = max(dp, default_subspace(max(dp, (min(k, MAX_P) + 15) // 16 * 16), k))
+    align = 32 if S.dtype == torch.float64 else 16
+    if dp != d or S.stride(1) != 1 or S.stride(0) % 4 or S.data_ptr() % align:
+        Sp = torch.zeros((dp, dp), dtype=S.dtype, device=S.device)
         Sp[:d, :d] = S
         S = Sp
     q, k0, ldq = _warm(q0, d, S.device)
@@ -301,24 +354,21 @@ def topk_eigh(S: torch.Tensor, k: int, *, p: int | None = None, tol: float = DEF
         qp[:d] = q
         q, ldq = qp.t().contiguous().t(), dp
     pp = int(p) if p else default_subspace(dp, k)
+    stype = _lib.DEIG_F64 if S.dtype == torch.float64 else _lib.DEIG_F32
+    o = opts if opts is not None else _lib.solver_opts()
     V = _colmajor(dp, k, S.device)
     evals = torch.empty(k, dtype=torch.float32, device=S.device)
     sweeps, resid = ctypes.c_int(0), ctypes.c_float(0)
     L = _lib.lib()
     with torch.cuda.device(S.device):
-        nbytes = L.deig_topk_workspace(dp, k, pp)
+        nbytes = L.deig_topk_workspace_ex(dp, k, pp, stype, ctypes.byref(o))
         ws = _workspace(S.device, nbytes)
-        rc = L.deig_topk_sym_f32(S.data_ptr(), dp, S.stride(0), k, pp, int(max_sweeps),
-                                 ctypes.c_float(tol), q.data_ptr() if q is not None else None,
-                                 k0, ldq, V.data_ptr(), dp, evals.data_ptr(),
-                                 ctypes.byref(sweeps), ctypes.byref(resid), ws.data_ptr(),
-                                 nbytes, _stream(S.device))
-    res = _finish(rc, V, evals, sweeps, resid, "deig_topk_sym_f32")
-    ev = res.evals
-    if float(ev[0]) < -1e-6 * float(ev.abs().max()):
-        warnings.warn("topk_eigh: negative eigenvalue returned - the input looks indefinite; the "
-                      "solver assumes a positive semi-definite matrix", IndefiniteWarning,
-                      stacklevel=2)
+        rc = L.deig_topk_sym_ex(S.data_ptr(), stype, dp, S.stride(0), k, pp, int(max_sweeps),
+                                ctypes.c_float(tol), q.data_ptr() if q is not None else None,
+                                k0, ldq, V.data_ptr(), dp, evals.data_ptr(),
+                                ctypes.byref(sweeps), ctypes.byref(resid), ctypes.byref(o),
+                                ws.data_ptr(), nbytes, _stream(S.device))
+    res = _finish(rc, V, evals, sweeps, resid, "deig_topk_sym_ex")
     if dp != d:
         res.V = res.V[:d].t().contiguous().t()
     return res
@@ -332,7 +382,8 @@ def stack_bases(bases) -> torch.Tensor:
 
 def projavg_topk(Wt: torch.Tensor, k: int, scale: float, *, p: int | None = None,
                  tol: float = DEFAULT_TOL, max_sweeps: int = DEFAULT_MAX_SWEEPS,
-                 q0: torch.Tensor | None = None) -> EigResult:
+                 q0: torch.Tensor | None = None,
+                 opts: "_lib.SolverOpts | None" = None) -> EigResult:
     """Top-k eigenpairs of scale * sum_i V_i V_i^T, never forming the d x d matrix.
 
     GPU replacement for MasterNode.callback_ (distributed.py:126-130:
@@ -347,11 +398,9 @@ def projavg_topk(Wt: torch.Tensor, k: int, scale: float, *, p: int | None = None
     k = int(k)
     if not 1 <= k <= d:
         raise ValueError(f"k={k} out of range [1, {d}]")
-    if k > MAX_K:
-        raise ValueError(f"k={k} > {MAX_K}: the GPU solver's subspace is capped at {MAX_K} columns")
     dp = _pad_dim(d)
     if not p:
-        dp = max(dp, default_subspace(max(dp, (k + 15) // 16 * 16), k))
+        dp = max(dp, default_subspace(max(dp, (min(k, MAX_P) + 15) // 16 * 16), k))
     if dp != d or Wt.stride(1) != 1 or Wt.stride(0) % 4 or Wt.data_ptr() % 16:
         Wp = torch.zeros((mk, dp), dtype=torch.float32, device=Wt.device)
         Wp[:, :d] = Wt
@@ -362,20 +411,21 @@ def projavg_topk(Wt: torch.Tensor, k: int, scale: float, *, p: int | None = None
         qp[:d] = q
         q, ldq = qp.t().contiguous().t(), dp
     pp = int(p) if p else default_subspace(dp, k)
+    o = opts if opts is not None else _lib.solver_opts()
     V = _colmajor(dp, k, Wt.device)
     evals = torch.empty(k, dtype=torch.float32, device=Wt.device)
     sweeps, resid = ctypes.c_int(0), ctypes.c_float(0)
     L = _lib.lib()
     with torch.cuda.device(Wt.device):
-        nbytes = L.deig_projavg_workspace(dp, mk, k, pp)
+        nbytes = L.deig_projavg_workspace_ex(dp, mk, k, pp, ctypes.byref(o))
         ws = _workspace(Wt.device, nbytes)
-        rc = L.deig_projavg_topk_f32(Wt.data_ptr(), dp, mk, Wt.stride(0), ctypes.c_float(scale),
-                                     k, pp, int(max_sweeps), ctypes.c_float(tol),
-                                     q.data_ptr() if q is not None else None, k0, ldq,
-                                     V.data_ptr(), dp, evals.data_ptr(), ctypes.byref(sweeps),
-                                     ctypes.byref(resid), ws.data_ptr(), nbytes,
-                                     _stream(Wt.device))
-    res = _finish(rc, V, evals, sweeps, resid, "deig_projavg_topk_f32")
+        rc = L.deig_projavg_topk_ex(Wt.data_ptr(), dp, mk, Wt.stride(0), ctypes.c_float(scale),
+                                    k, pp, int(max_sweeps), ctypes.c_float(tol),
+                                    q.data_ptr() if q is not None else None, k0, ldq,
+                                    V.data_ptr(), dp, evals.data_ptr(), ctypes.byref(sweeps),
+                                    ctypes.byref(resid), ctypes.byref(o), ws.data_ptr(), nbytes,
+                                    _stream(Wt.device))
+    res = _finish(rc, V, evals, sweeps, resid, "deig_projavg_topk_ex")
     if dp != d:
         res.V = res.V[:d].t().contiguous().t()
     return res

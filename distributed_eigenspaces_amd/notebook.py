@@ -40,8 +40,15 @@ def compute_segma_hat(x):
 
 
 def _worker_basis(x, k: int) -> torch.Tensor:
-    """One worker: GPU Sigma_hat then top-k; returns V (d x k, column-major, device)."""
-    S = linalg.sigma_hat(linalg.require_device_tensor(x, "batch"))
+    """One worker: GPU Sigma_hat then top-k; returns V (d x k, column-major, device).
+    float64 batches (the notebook's data.mean(axis=3) values, NB:54) take the
+    mean-shifted float64 covariance; uint8 the exact one; float32 the fp32 SYRK."""
+    if not isinstance(x, torch.Tensor):
+        x = torch.as_tensor(np.asarray(x))
+    if x.dtype == torch.uint8:
+        S = linalg.sigma_hat(x, dtype=torch.float64)
+    else:
+        S = linalg.sigma_hat(linalg.require_device_tensor(x, "batch", keep_f64=True))
     return linalg.topk_eigh(S, k, check_finite=False).V
 
 
@@ -111,7 +118,7 @@ def online_distributed_pca(batches=None, m: int = 10, T: int = 10, k: int = 2,
 def one_shot_distributed_pca(data, k: int, batches_number: int):
     """distributed.py master/slave pipeline in one call: contiguous shards of N // M
     rows (remainder dropped, :99-104), worker top-k, implicit server solve."""
-    x = linalg.require_device_tensor(data, "data")
+    x = linalg.require_device_tensor(data, "data", keep_f64=True)
     step = x.shape[0] // batches_number
     bases = [_worker_basis(x[i * step:(i + 1) * step], k) for i in range(batches_number)]
     Wt = linalg.stack_bases(bases)

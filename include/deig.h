@@ -35,7 +35,11 @@ extern "C" {
 #define DEIG_EHIP (-2)
 #define DEIG_EWORKSPACE (-3)
 
-/* Library version, e.g. 0x000100 for 0.1.0. */
+/* Element types of float inputs (deig_syrk_shift, deig_topk_sym_ex). */
+#define DEIG_F32 0
+#define DEIG_F64 1
+
+/* Library version, e.g. 0x000300 for 0.3.0. */
 int deig_version(void);
 
 /* Thread-local message for the last nonzero return on this thread ("" if none). */
@@ -71,6 +75,24 @@ int deig_syrk_f32_ex(const float* X, int64_t n, int64_t d, int64_t ldx, float al
                      float* S, int64_t lds, int algo, void* ws, size_t ws_bytes, void* stream);
 size_t deig_syrk_workspace_ex(int64_t n, int64_t d, int algo);
 
+/* Mean-shifted covariance of float samples, float64 result (the reference's own
+ * float64 data flow: distributed.py:169-173 grey values -> compute_sigma_hat_
+ * :59-70):  S64 = alpha * X^T X  computed as
+ *   alpha [ C^T C + s mu^T + mu s^T + n mu mu^T ],  mu = column means (double),
+ *   C = fl32(X - mu), s = sum_r (x_r - mu) (double)
+ * with C^T C on the split3 / fp32 SYRK (n >= / < DEIG_SYRK_SPLIT_MIN_ROWS): the
+ * SYRK's rounding is then relative to the CENTRED data, not to the mean direction
+ * that dominates an uncentered covariance of byte images (see shift.hip for the
+ * measured effect on the top-k basis).  X: n x d row-major, element type xtype
+ * (DEIG_F32 / DEIG_F64), row stride ldx elements, aligned to its element size.
+ * S64 (float64, lds64) and/or S (its fp32 rounding, lds) may be NULL (not both);
+ * both triangles are written (bit-exact symmetry).
+ * Workspace: deig_syrk_shift_workspace(n, d, xtype) (holds an fp32 copy of C). */
+int deig_syrk_shift(const void* X, int xtype, int64_t n, int64_t d, int64_t ldx, double alpha,
+                    double* S64, int64_t lds64, float* S, int64_t lds, void* ws, size_t ws_bytes,
+                    void* stream);
+size_t deig_syrk_shift_workspace(int64_t n, int64_t d, int xtype);
+
 /* Exact covariance of uint8 samples (fused ingest):
  *   S = alpha * V^T V,  V the n x d feature matrix of
  *   DEIG_U8_RAW:   v = x, the first d bytes of each row (e.g. raw CIFAR rows, d = 3072);
@@ -79,9 +101,10 @@ size_t deig_syrk_workspace_ex(int64_t n, int64_t d, int algo);
  *                  (data.mean(axis=3), reshape), fused into the covariance.
  * Replaces compute_sigma_hat_ (distributed.py:59-70) on the uint8 CIFAR bytes of
  * load_data.py:18-33 (alpha = 1/n reproduces the reference).  Every product and
- * sum is exact (int8 MFMA with int32 accumulation, int64 combination), so S is the
- * correctly rounded fp32 value (S64: the fp64 value, optional, may be NULL; S may be
- * NULL when S64 is given) of the reference's float64 result; both triangles are
+ * sum is exact (int8 MFMA with int32 accumulation, int64 combination), so S64 is the
+ * reference's float64 result rounded once (alpha = 1/n: one division of the exact
+ * integer sum) and S its fp32 rounding (within 1 ulp of the correctly rounded
+ * value); either may be NULL (not both); both triangles are
  * written (bit-exact symmetry).  Requires d % 4 == 0, d <= 32768, ldx % 4 == 0 bytes,
  * X 4-byte aligned.  Workspace: deig_syrk_u8_workspace(n, d, mode). */
 #define DEIG_U8_RAW 0
@@ -101,8 +124,7 @@ int deig_default_subspace(int64_t d, int k);
  *    bytes of S for every p <= 128;
  *  DEIG_SWEEP_FP32: f32 MFMA skinny kernel (exact fp32 fma chain, f32-MFMA-bound
  *    above p ~ 40);
- *  DEIG_SWEEP_AUTO: BF16X6.  deig_topk_sym_f32 uses AUTO unless the environment
- *    sets DEIG_SWEEP_ALGO=fp32. */
+ *  DEIG_SWEEP_AUTO: BF16X6 (the solvers' default; deig_solver_opts.sweep_algo). */
 #define DEIG_SWEEP_AUTO 0
 #define DEIG_SWEEP_BF16X6 1
 #define DEIG_SWEEP_FP32 2
@@ -151,22 +173,49 @@ int deig_sym_power_f32(const float* S, int64_t d, int64_t lds, float* Q, int p, 
                        float* Y, int64_t ldy, const float* cs, int steps, int algo, void* ws,
                        size_t ws_bytes, void* stream);
 
+/* Options of the eigensolvers (deig_topk_sym_ex, deig_projavg_topk_ex).  Fill with
+ * deig_solver_opts_init() and change fields; NULL options = the defaults.  These
+ * replace the r02 environment knobs: the library reads no environment variables. */
+typedef struct deig_solver_opts {
+  int size;                  /* sizeof(deig_solver_opts), set by deig_solver_opts_init */
+  int sweep_algo;            /* DEIG_SWEEP_AUTO (bf16x6 sweeps over an image of S) or
+                                DEIG_SWEEP_FP32 (f32-MFMA skinny products; float32 S only) */
+  int rr_every;              /* sweeps per Rayleigh-Ritz step before the Chebyshev filter
+                                starts (0: 4 with >= 16 guard columns, else 2) */
+  int chebyshev;             /* 1 (default): Chebyshev filter once resid <= cheb_above */
+  float cheb_above;          /* 1e-2 */
+  int deflate;               /* 1 (default): lock dominant pairs (theta_1 >= 64 theta_k) and
+                                iterate the rest on the deflated operator */
+  int deflate_early;         /* 1 (default): lock them as soon as they are converged */
+  int jacobi_early_sweeps;   /* Jacobi sweeps of early Rayleigh-Ritz steps (-1: 2 explicit S,
+                                3 projector average; 0: uncapped) */
+  float jacobi_early_above;  /* residual above which the cap applies (< 0: 1e-4 / 1e-2) */
+  float fast_until;          /* three-product sweeps while resid > this (1e-3; 0: never) */
+  float round_until;         /* five-product sweeps while resid > this (1e-4) */
+  int debug;                 /* 1: per-Rayleigh-Ritz trace on stderr */
+} deig_solver_opts;
+void deig_solver_opts_init(deig_solver_opts* opts);
+
 /* Top-k eigenpairs of a dense symmetric S (d x d, row-major, lds), ascending.
  * Replaces Node.top_k_eigenvectors  distributed.py:22-29
  * (scipy.linalg.eigh(S, eigvals=(d-k, d-1))[1]  ->  LAPACK dsyevr), plus the
  * eigenvalues ([0] of the same call) as a side output.
+ * Any 1 <= k <= d and any symmetric S, like ?syevr.
  * Block subspace iteration with Rayleigh-Ritz on a p-dimensional subspace
- * (k <= p <= 128, p % 16 == 0, p <= d); between Rayleigh-Ritz steps a scaled
- * Chebyshev filter on [0, c] (c from the Ritz values; power steps while the
- * residual is above 1e-2) - S must be positive semi-definite, as covariances and
- * projector averages are.  When theta_1 >= 64 theta_k (an uncentered covariance's
- * mean direction), a second stage iterates the other pairs on S - V_D L_D V_D^T
- * (fp32 products S q would otherwise lose their digits to cancellation).  Q0
- * (d x k0 column-major, ldq0) is an optional warm start (NULL / k0 = 0 ->
+ * (k <= p <= 128, p % 16 == 0, p <= d; k > 128: blocks of p - 16 pairs on a p-column
+ * subspace, p = 128 by default, each block's pairs LOCKED and deflated out of S for
+ * the blocks below); between Rayleigh-Ritz steps a scaled Chebyshev filter on [0, c]
+ * (c from the Ritz values; power steps while the residual is above 1e-2).  An
+ * indefinite S is detected by the Ritz values (a negative one of significant size)
+ * and solved as S + sigma I (the eigenvalues returned are S's).  When theta_1 >=
+ * 64 theta_k (an uncentered covariance's mean direction), the dominant pairs are
+ * locked and the others iterated on S - V_D L_D V_D^T (formed in double: fp32
+ * products S q would otherwise lose their digits to cancellation).  Q0 (d x k0
+ * column-major, ldq0) is an optional warm start for k <= 128 (NULL / k0 = 0 ->
  * deterministic pseudo-random start).  Stops when
  * max_j ||S v_j - lambda_j v_j|| <= tol * |lambda_max| (or the residual stalls
  * within 4 tol / 2e-6 of it, the fp32 floor); returns DEIG_NOT_CONVERGED after
- * max_sweeps sweeps, or earlier when it stalls above that floor.
+ * max_sweeps sweeps (per block), or earlier when it stalls above that floor.
  * Outputs: V (d x k col-major, ldv), evals (k, ascending), *sweeps_out,
  * *resid_out = final max relative residual (host pointers, may be NULL). */
 int deig_topk_sym_f32(const float* S, int64_t d, int64_t lds, int k, int p,
@@ -174,6 +223,15 @@ int deig_topk_sym_f32(const float* S, int64_t d, int64_t lds, int k, int p,
                       float* V, int64_t ldv, float* evals, int* sweeps_out,
                       float* resid_out, void* ws, size_t ws_bytes, void* stream);
 size_t deig_topk_workspace(int64_t d, int k, int p);
+/* The same for S of element type stype (DEIG_F32 / DEIG_F64: a float64 S - the
+ * reference's dtype - is read in double by the image pass and the deflation, so
+ * the small eigenvectors of an uncentered covariance keep float64 parity), with
+ * options (NULL: defaults). */
+int deig_topk_sym_ex(const void* S, int stype, int64_t d, int64_t lds, int k, int p, int max_sweeps,
+                     float tol, const float* Q0, int k0, int64_t ldq0, float* V, int64_t ldv,
+                     float* evals, int* sweeps_out, float* resid_out, const deig_solver_opts* opts,
+                     void* ws, size_t ws_bytes, void* stream);
+size_t deig_topk_workspace_ex(int64_t d, int k, int p, int stype, const deig_solver_opts* opts);
 
 /* Server solve: top-k eigenpairs of  scale * sum_i V_i V_i^T  without forming it.
  * Wt = [V_1^T; ...; V_m^T] is (mk) x d row-major (ldw); scale = 1/batches_number.
@@ -187,6 +245,13 @@ int deig_projavg_topk_f32(const float* Wt, int64_t d, int64_t mk, int64_t ldw,
                           float* evals, int* sweeps_out, float* resid_out, void* ws,
                           size_t ws_bytes, void* stream);
 size_t deig_projavg_workspace(int64_t d, int64_t mk, int k, int p);
+/* With options (k > 128: block locking with the locked pairs deflated by products
+ * with them - the operator stays implicit). */
+int deig_projavg_topk_ex(const float* Wt, int64_t d, int64_t mk, int64_t ldw, float scale, int k,
+                         int p, int max_sweeps, float tol, const float* Q0, int k0, int64_t ldq0,
+                         float* V, int64_t ldv, float* evals, int* sweeps_out, float* resid_out,
+                         const deig_solver_opts* opts, void* ws, size_t ws_bytes, void* stream);
+size_t deig_projavg_workspace_ex(int64_t d, int64_t mk, int k, int p, const deig_solver_opts* opts);
 
 /* One mini-batch Oja step (online variant, BASELINE.json config 4; not in the
  * reference - parity unpinned):  V <- orth(V + eta/b * Xb^T (Xb V)).

@@ -235,6 +235,10 @@ def main():
         # p = k, no guard columns): one 32768-row shard; the worker outputs only,
         # stored as float32 (16 MB of float64 otherwise; the tests' bars are 1e-4 / 1e-5)
         ("spiked_d16384_k128_m1_seeded", 32768, 16384, 128, 1, 18, False, False),
+        # config-3's server leg: m = 8 shards of 8192 rows at d = 8192, k = 64 (the
+        # 8-basis projector average of distributed.py:126-130 + NB:306); stores the
+        # server outputs, every worker's eigenvalues and shard 0's basis (float32)
+        ("spiked_d8192_k64_m8_seeded", 8 * 8192, 8192, 64, 8, 19, False, False),
     ]
     only = set(sys.argv[1:])  # optional: regenerate just the named cases
     for name, n, d, k, m, seed, proto, store_s in cases:
@@ -254,6 +258,9 @@ def main():
                 out.pop("U_planted")  # regenerable from the seed; keeps the fixture small
             if d > 8192:
                 out["worker_V"] = out["worker_V"].astype(np.float32)
+            if m > 1 and d >= 8192:  # keep the fixture small: shard 0's basis only
+                out["worker_V"] = out["worker_V"][:1].astype(np.float32)
+                out["server_V"] = out["server_V"].astype(np.float32)
             out.update(seed=np.int64(seed), n=np.int64(n), d=np.int64(d),
                        xq_sha256=np.array(xq_digest(Xq)))
         if (not store_s or d > 256) and "sigma_tilde" in out:

@@ -35,7 +35,7 @@ def test_header_constants_match_bindings():
 
 def test_version_and_error_string():
     L = _lib.lib()
-    assert L.deig_version() == 0x000100
+    assert L.deig_version() == 0x000300
     assert isinstance(_lib.last_error(), str)
 
 
@@ -89,14 +89,57 @@ def test_no_cpu_fallback():
         de.topk_eigh(torch.eye(16), 2)
 
 
-def test_workspace_fused_split_variant(monkeypatch):
-    """d <= 4096 (config 2) defaults to the fused split, which stages X itself: no
-    image of the shard in the workspace; DEIG_SYRK_VARIANT=162 brings it back."""
+def test_workspace_fused_split_variant():
+    """d <= 4096 (config 2) uses the fused split, which stages X itself: no image of
+    the shard in the workspace; d > 4096 keeps the split pass and its image."""
     L = _lib.lib()
     n, d = 1 << 20, 3072
     ws = L.deig_syrk_workspace_ex(n, d, _lib.DEIG_SYRK_SPLIT3)
     assert 0 < ws < n * d * 4 // 10  # slabs only (the image would be n * d * 4)
-    monkeypatch.setenv("DEIG_SYRK_VARIANT", "162")
-    assert L.deig_syrk_workspace_ex(n, d, _lib.DEIG_SYRK_SPLIT3) >= n * d * 4
-    monkeypatch.setenv("DEIG_SYRK_VARIANT", "163")
-    assert L.deig_syrk_workspace_ex(1 << 21, 8192, _lib.DEIG_SYRK_SPLIT3) < (1 << 30)
+    assert L.deig_syrk_workspace_ex(1 << 21, 8192, _lib.DEIG_SYRK_SPLIT3) >= (1 << 21) * 8192 * 4
+
+
+def test_solver_opts_struct_and_defaults():
+    """deig_solver_opts: the ctypes mirror has the C size (the library checks it) and
+    the defaults the r02 environment knobs had."""
+    o = _lib.solver_opts()
+    assert o.size == ctypes.sizeof(_lib.SolverOpts)
+    assert (o.chebyshev, o.deflate, o.deflate_early, o.rr_every) == (1, 1, 1, 0)
+    assert abs(o.cheb_above - 1e-2) < 1e-9 and abs(o.fast_until - 1e-3) < 1e-9
+    assert abs(o.round_until - 1e-4) < 1e-9 and o.jacobi_early_sweeps == -1
+    bad = _lib.SolverOpts()
+    bad.size = 4
+    V = ctypes.c_int(0)
+    rc = _lib.lib().deig_topk_sym_ex(16, _lib.DEIG_F32, 64, 64, 2, 16, 10, ctypes.c_float(1e-6),
+                                     None, 0, 0, 16, 64, 16, ctypes.byref(V), None,
+                                     ctypes.byref(bad), 16, 1 << 20, None)
+    assert rc == _lib.DEIG_EINVAL and "size" in _lib.last_error()
+
+
+def test_library_reads_no_environment():
+    """No A/B knobs in the shipped library: no getenv in csrc/, none imported by the .so."""
+    import os
+    import shutil
+    import subprocess
+    csrc = os.path.join(os.path.dirname(_lib.HERE), "distributed_eigenspaces_amd", "csrc")
+    for f in os.listdir(csrc):
+        assert "getenv" not in open(os.path.join(csrc, f)).read(), f
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    if os.path.exists(nm):
+        out = subprocess.run([nm, "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True,
+                             text=True).stdout
+        assert "getenv" not in out
+
+
+def test_general_k_and_shift_workspaces():
+    """k > 128 (block locking) and the mean-shifted covariance have workspace queries."""
+    L = _lib.lib()
+    assert L.deig_default_subspace(3072, 256) == 128
+    assert L.deig_default_subspace(1024, 200) == 128
+    o = _lib.solver_opts()
+    w256 = L.deig_topk_workspace_ex(3072, 256, 0, _lib.DEIG_F64, ctypes.byref(o))
+    assert w256 >= L.deig_topk_workspace(3072, 112, 128) > 0
+    assert L.deig_projavg_workspace_ex(3072, 8 * 256, 256, 0, ctypes.byref(o)) > 0
+    n, d = 7500, 1024
+    ws = L.deig_syrk_shift_workspace(n, d, _lib.DEIG_F64)
+    assert ws >= n * d * 4 + d * d * 4  # fp32 copy of X - mu and the centred image

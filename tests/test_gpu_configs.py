@@ -173,3 +173,29 @@ def test_c5_server_64_bases_d16384_k128(cuda):
     w, Vr = _topk64_subspace(op, d, k, 160, 12, cuda)
     np.testing.assert_allclose(ev.cpu().numpy(), w.cpu().numpy(), rtol=EV_TOL)
     assert ref_cpu.projector_distance(V.cpu().numpy(), Vr.cpu().numpy()) <= P_TOL
+
+
+def test_c3_server_leg_m8_golden(cuda):
+    """configs[2]'s server leg on one GPU: the 8-basis projector average at d = 8192,
+    k = 64 (distributed.py:126-130 + NB:306) from 8 logical workers' bases, against
+    the reference's own run (tests/golden spiked_d8192_k64_m8_seeded: 8 shards of 8192
+    rows through distributed.py's SlaveNode math, the master's sigma_tilde and the
+    notebook's server solve).  End to end through the estimator (one rank, 8
+    workers): shard 0's basis and every worker's eigenvalues, then the server basis
+    and its eigenvalues."""
+    from distributed_eigenspaces_amd.estimator import DistributedEigenspaceEstimator
+    from tests.conftest import load_golden
+    g = load_golden("spiked_d8192_k64_m8_seeded")
+    k, m = int(g["k"]), int(g["m"])
+    X = torch.from_numpy(g["Xq"]).to(cuda).float() / float(g["grid"])
+    est = DistributedEigenspaceEstimator(k, workers_per_rank=m)
+    r = est.fit(X)
+    torch.cuda.synchronize()
+    for i in range(m):
+        np.testing.assert_allclose(r.worker_evals[i].double().cpu().numpy(), g["worker_evals"][i],
+                                   rtol=EV_TOL)
+    V0 = r.Wt[:k].t().double().cpu().numpy()
+    assert ref_cpu.projector_distance(V0, g["worker_V"][0]) <= P_TOL
+    dist = ref_cpu.projector_distance(r.V.cpu().numpy(), g["server_V"])
+    assert dist <= P_TOL, dist
+    np.testing.assert_allclose(r.evals.double().cpu().numpy(), g["server_evals"], rtol=EV_TOL)

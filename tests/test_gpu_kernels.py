@@ -149,10 +149,10 @@ def test_worker_path_golden(name, algo, cuda):
         r = de.topk_eigh(S, k)
         V = r.V.cpu().numpy().astype(np.float64)
         ev = r.evals.cpu().numpy().astype(np.float64)
-        Vr, evr = g["worker_V"][i], g["worker_evals"][i]
-        dist = ref_cpu.projector_distance(V, Vr)
-        assert dist <= P_TOL, f"{name} shard {i}: ||P-P_ref||_F = {dist:.3e}"
-        np.testing.assert_allclose(ev, evr, rtol=EV_TOL, atol=0)
+        if i < len(g["worker_V"]):  # m = 8 at d = 8192: shard 0's basis is stored
+            dist = ref_cpu.projector_distance(V, g["worker_V"][i])
+            assert dist <= P_TOL, f"{name} shard {i}: ||P-P_ref||_F = {dist:.3e}"
+        np.testing.assert_allclose(ev, g["worker_evals"][i], rtol=EV_TOL, atol=0)
         assert r.V.stride() == (1, V.shape[0])  # Fortran order like LAPACK
 
 
@@ -164,6 +164,9 @@ def test_server_golden(name, cuda):
         pytest.skip("fixture stores the worker outputs only (d = 16384)")
     g = load_golden(name)
     k, m = int(g["k"]), int(g["m"])
+    if len(g["worker_V"]) < m:
+        pytest.skip("fixture stores shard 0's basis only: see test_gpu_configs "
+                    "test_c3_server_leg_m8_golden for the end-to-end server check")
     bases = [torch.from_numpy(v.astype(np.float32)).to(cuda) for v in g["worker_V"]]
     Wt = de.stack_bases(bases)
     r = de.projavg_topk(Wt, k, 1.0 / m, q0=bases[0])

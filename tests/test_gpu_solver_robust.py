@@ -141,19 +141,27 @@ def test_k_close_to_small_d(d, k, cuda):
     np.testing.assert_allclose(r.evals.cpu().numpy(), w, rtol=EV_TOL)
 
 
-def test_indefinite_input_warns(cuda):
-    """The solver assumes PSD (documented); a negative returned eigenvalue warns."""
+def test_indefinite_top_k_reaches_negative_eigenvalues(cuda):
+    """Indefinite S whose top-k algebraic pairs include negative eigenvalues (eigh
+    returns them; r02 warned instead): detected from the Ritz values and solved on
+    S + sigma I, eigenvalues returned unshifted."""
     import distributed_eigenspaces_amd as de
-    from distributed_eigenspaces_amd.linalg import IndefiniteWarning
     d, k = 64, 8
-    lams = np.concatenate([np.linspace(2.0, 1.0, 4), -np.linspace(0.5, 0.1, d - 4)])
+    lams = np.concatenate([[2.0, 1.5, 1.2, 1.0], -np.linspace(0.1, 0.16, 4),
+                           -np.linspace(0.5, 3.0, d - 8)])
     S = _matrix(lams, seed=9)
-    with pytest.warns(IndefiniteWarning):
-        de.topk_eigh(torch.from_numpy(S).to(cuda), k)
+    r = de.topk_eigh(torch.from_numpy(S).to(cuda), k)
+    assert r.converged
+    w, V = ref_cpu.top_k_eigh(S.astype(np.float64), k)
+    assert w[0] < 0
+    assert ref_cpu.projector_distance(r.V.cpu().numpy(), V) <= P_TOL
+    np.testing.assert_allclose(r.evals.cpu().numpy(), w, rtol=EV_TOL, atol=1e-6)
 
 
-def test_k_above_cap_is_a_clear_error(cuda):
+def test_k_outside_range_is_a_clear_error(cuda):
     import distributed_eigenspaces_amd as de
     S = torch.eye(256, device=cuda)
-    with pytest.raises(ValueError, match="capped at 128"):
-        de.topk_eigh(S, 129)
+    with pytest.raises(ValueError, match="out of range"):
+        de.topk_eigh(S, 257)
+    with pytest.raises(ValueError, match="out of range"):
+        de.topk_eigh(S, 0)

@@ -99,3 +99,69 @@ def test_address_parsing():
     assert br.parse_address("tcp://rabbit") == ("rabbit", 5672)
     assert br.parse_address("localhost:5673") == ("localhost", 5673)
     assert br.parse_address("inproc-name") is None
+
+
+def test_cli_bare_broker_host_is_the_socket_broker():
+    """The reference's CLI form ``--broker localhost`` (a RabbitMQ host name,
+    distributed.py:16, :158): in master / slave mode it means the socket broker on
+    that host at pika's port 5672 - an in-process broker per process would never
+    connect the two."""
+    import socket
+
+    from distributed_eigenspaces_amd import distributed as dd
+    assert dd.cli_broker("localhost", "slave") == "tcp://localhost:5672"
+    assert dd.cli_broker("10.0.0.7", "master") == "tcp://10.0.0.7:5672"
+    assert dd.cli_broker("tcp://h:1234", "master") == "tcp://h:1234"
+    assert dd.cli_broker("h:1234", "slave") == "h:1234"
+    assert dd.cli_broker("inproc-x", "local") == "inproc-x"
+    try:
+        b = br.SocketBroker("127.0.0.1", 5672).start()
+    except OSError:
+        pytest.skip("port 5672 busy")
+    try:
+        pub = br.connect(dd.cli_broker("127.0.0.1", "master")).channel()
+        sub = br.connect(dd.cli_broker("127.0.0.1", "slave")).channel()
+        sub.queue_declare("slaves")
+        seen = []
+
+        def cb(ch, m, p, body):
+            seen.append(body.decode())
+            ch.basic_ack(m.delivery_tag)
+            ch.stop_consuming()
+        sub.basic_consume("slaves", cb)
+        pub.basic_publish("", "slaves", '{"rank": 2, "batch": [0, 10]}')
+        sub.start_consuming()
+        assert seen == ['{"rank": 2, "batch": [0, 10]}']
+    finally:
+        b.shutdown()
+    del socket
+
+
+def test_slow_consumer_does_not_block_the_broker():
+    """A consumer that never reads its deliveries (large bodies fill its socket
+    buffers) must not stall other connections: deliveries are written by per-client
+    sender threads, outside the broker lock."""
+    b = br.SocketBroker("127.0.0.1", 0).start()
+    try:
+        stuck = br.connect(b.address).channel()
+        stuck.basic_consume("big", lambda *a: None)  # never reads
+        pub = br.connect(b.address).channel()
+        body = "x" * (4 << 20)
+        for _ in range(8):  # 32 MB queued towards the stuck consumer
+            pub.basic_publish("", "big", body)
+        other = br.connect(b.address).channel()
+        seen = []
+
+        def cb(ch, m, p, bd):
+            seen.append(bd.decode())
+            ch.basic_ack(m.delivery_tag)
+            ch.stop_consuming()
+        other.basic_consume("small", cb)
+        pub.basic_publish("", "small", "ping")
+        import threading
+        t = threading.Thread(target=other.start_consuming, daemon=True)
+        t.start()
+        t.join(timeout=20)
+        assert seen == ["ping"]
+    finally:
+        b.shutdown()

@@ -1,0 +1,98 @@
+"""A/B timing of covariance SYRK builds in ONE process (interleaved rounds, same
+device, same data; cdna_hip_programming.md §5.4 rule 24).  Measurement tooling only:
+the variants are separate builds of libdeig.so with -DDEIG_AB_SYRK_VARIANT=N (the
+shipped library has no knobs).
+
+  python tools/syrk_ab.py build 162 174            # here (CPU): tools/ab_libs/libdeig_v*.so
+  python tools/syrk_ab.py run 162 174 [--n N --d D --rounds R]   # on the GPU box
+"""
+import argparse
+import ctypes
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+LIBDIR = os.path.join(ROOT, "tools", "ab_libs")
+
+
+def lib_path(v):
+    return os.path.join(LIBDIR, f"libdeig_v{v}.so")
+
+
+def build(variants):
+    from distributed_eigenspaces_amd import _build
+    os.makedirs(LIBDIR, exist_ok=True)
+    for v in variants:
+        _build.build_library(force=True, defines=[f"-DDEIG_AB_SYRK_VARIANT={v}"], out=lib_path(v))
+
+
+def run(variants, n, d, rounds, reps):
+    import torch
+
+    from distributed_eigenspaces_amd import _lib, synthetic
+    dev = torch.device("cuda", 0)
+    libs = {}
+    for v in variants:
+        L = ctypes.CDLL(lib_path(v))
+        for name in ("deig_syrk_f32_ex", "deig_syrk_workspace_ex", "deig_last_error"):
+            res, args = _lib.SIGNATURES[name]
+            getattr(L, name).restype = res
+            getattr(L, name).argtypes = args
+        libs[v] = L
+    U = synthetic.planted_basis(d, 64, seed=0, device=dev)
+    X = synthetic.spiked_samples(n, U, seed=1)
+    nbytes = max(L.deig_syrk_workspace_ex(n, d, _lib.DEIG_SYRK_SPLIT3) for L in libs.values())
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    S = {v: torch.empty((d, d), dtype=torch.float32, device=dev) for v in variants}
+    st = torch.cuda.current_stream(dev)
+
+    def launch(v):
+        rc = libs[v].deig_syrk_f32_ex(X.data_ptr(), n, d, d, ctypes.c_float(1.0 / n), S[v].data_ptr(),
+                                      d, _lib.DEIG_SYRK_SPLIT3, ws.data_ptr(), nbytes, st.cuda_stream)
+        if rc:
+            raise RuntimeError(f"v{v}: {libs[v].deig_last_error()}")
+
+    for v in variants:  # warm-up (clock, caches)
+        launch(v)
+    torch.cuda.synchronize()
+    times = {v: [] for v in variants}
+    for r in range(rounds):
+        for v in variants:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(reps):
+                launch(v)
+            e1.record(st)
+            e1.synchronize()
+            times[v].append(e0.elapsed_time(e1) / reps)
+        print(f"round {r}: " + "  ".join(f"v{v} {times[v][-1]:.2f} ms" for v in variants), flush=True)
+    flop = 3.0 * n * d * (d + 1)
+    base = variants[0]
+    for v in variants:
+        med = statistics.median(times[v])
+        diff = (S[v] - S[base]).abs().max().item() / S[base].abs().max().item()
+        print(f"v{v}: median {med:.2f} ms min {min(times[v]):.2f} ms = "
+              f"{flop / med / 1e9:.1f} TF/s bf16 ({flop / med / 1e9 / 2500:.3f} of 2.5 PF); "
+              f"max|S - S_v{base}|/max|S| = {diff:.2e}; symmetric {bool(torch.equal(S[v], S[v].t()))}",
+              flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cmd", choices=["build", "run"])
+    ap.add_argument("variants", nargs="+", type=int)
+    ap.add_argument("--n", type=int, default=1 << 21)
+    ap.add_argument("--d", type=int, default=8192)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=2)
+    a = ap.parse_args()
+    if a.cmd == "build":
+        build(a.variants)
+    else:
+        run(a.variants, a.n, a.d, a.rounds, a.reps)
+
+
+if __name__ == "__main__":
+    main()
