@@ -25,6 +25,7 @@ DEIG_EWORKSPACE = -3
 DEIG_SYRK_AUTO = 0
 DEIG_SYRK_SPLIT3 = 1
 DEIG_SYRK_FP32 = 2
+DEIG_SYRK_ACCUMULATE = 0x100
 SYRK_ALGOS = {"auto": DEIG_SYRK_AUTO, "split3": DEIG_SYRK_SPLIT3, "fp32": DEIG_SYRK_FP32}
 DEIG_SWEEP_AUTO = 0
 DEIG_SWEEP_BF16X6 = 1

@@ -132,6 +132,7 @@ struct SolverWs {
   float* Zt;
   float* T;     // d x p: X_{j-1} of the Chebyshev recurrence
   float* Tdef;  // k x p: Vd^T Q of the plain-product deflation
+  void* rq;     // partial sums of the final double-precision Rayleigh quotients
   float* slab;
   size_t slab_bytes;
   void* sweep_ws;  // bf16x6 sweep image (explicit S only)
@@ -158,6 +159,7 @@ SolverWs carve_solver(void* ws, size_t cap, int64_t d, int kb, int k, int p, int
   w.Zt = mk > 0 ? c.take<float>((size_t)mk * p) : nullptr;
   w.T = c.take<float>((size_t)d * p);
   w.Tdef = image ? nullptr : c.take<float>((size_t)k * p);
+  w.rq = mk > 0 ? nullptr : c.take<char>(rq_workspace_bytes(d));
   size_t sb = skinny_workspace_bytes(2 * p, 2 * p, d);  // Gram
   auto need = [&](int64_t M, int64_t N, int64_t K) {
     const size_t b = skinny_workspace_bytes(M, N, K);
@@ -624,7 +626,12 @@ int solve(const Operator& op0, int64_t d, int k, int p, int max_sweeps, float to
     }
     if (rc || !restart) break;
   }
-  if (!rc && shift != 0.0) rc = unshift_launch(evals, k, shift, st);
+  // eigenvalues: double-precision Rayleigh quotients on S itself (explicit S; they
+  // need no unshift), the projector average's fp32 Ritz values unshifted
+  if (!rc && !op0.implicit)
+    rc = rq_launch(op0.S, op0.stype, d, op0.lds, V, ldv, k, evals, sv.w.rq, st);
+  else if (!rc && shift != 0.0)
+    rc = unshift_launch(evals, k, shift, st);
   if (sweeps_out) *sweeps_out = sv.it;
   if (resid_out) *resid_out = rc ? sv.last : worst;
   if (rc) return rc;
@@ -675,7 +682,7 @@ static int syrk_resolve(int64_t n, int algo) {
 }
 
 size_t deig_syrk_workspace_ex(int64_t n, int64_t d, int algo) {
-  algo = syrk_resolve(n, algo);
+  algo = syrk_resolve(n, algo & ~DEIG_SYRK_ACCUMULATE);
   if (algo == DEIG_SYRK_FP32) return syrk_workspace_bytes(n, d);
   if (algo == DEIG_SYRK_SPLIT3) return syrk_split_workspace_bytes(n, d);
   return 0;
@@ -684,11 +691,14 @@ size_t deig_syrk_workspace_ex(int64_t n, int64_t d, int algo) {
 int deig_syrk_f32_ex(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha, float* S,
                      int64_t lds, int algo, void* ws, size_t ws_bytes, void* stream) {
   g_err[0] = 0;
-  algo = syrk_resolve(n, algo);
+  const bool acc = (algo & DEIG_SYRK_ACCUMULATE) != 0;
+  algo = syrk_resolve(n, algo & ~DEIG_SYRK_ACCUMULATE);
+  if (acc && algo != DEIG_SYRK_SPLIT3)
+    return fail(DEIG_EINVAL, "syrk: DEIG_SYRK_ACCUMULATE needs the split3 algorithm");
   if (algo == DEIG_SYRK_FP32)
     return syrk_launch(X, n, d, ldx, alpha, S, lds, ws, ws_bytes, (hipStream_t)stream);
   if (algo == DEIG_SYRK_SPLIT3)
-    return syrk_split_launch(X, n, d, ldx, alpha, S, lds, ws, ws_bytes, (hipStream_t)stream);
+    return syrk_split_launch(X, n, d, ldx, alpha, S, lds, ws, ws_bytes, (hipStream_t)stream, acc);
   return fail(DEIG_EINVAL, "syrk: unknown algorithm %d", algo);
 }
 

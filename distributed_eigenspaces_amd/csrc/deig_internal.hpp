@@ -70,8 +70,10 @@ int syrk_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha, 
                 int64_t lds, void* ws, size_t ws_bytes, hipStream_t stream);
 // Split-bf16 covariance SYRK (syrk_split.hip).
 size_t syrk_split_workspace_bytes(int64_t n, int64_t d);
+// accumulate: S += alpha X^T X (row chunks of one long shard, or several shards).
 int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha, float* S,
-                      int64_t lds, void* ws, size_t ws_bytes, hipStream_t stream);
+                      int64_t lds, void* ws, size_t ws_bytes, hipStream_t stream,
+                      bool accumulate = false);
 
 // Mean-shifted covariance of float samples (shift.hip); xtype DEIG_F32 / DEIG_F64.
 size_t syrk_shift_workspace_bytes(int64_t n, int64_t d, int xtype);
@@ -163,6 +165,10 @@ int rr_update_launch(const RRBuffers& b, int64_t d, int p, int k, float* V, int6
 int deflate_orth_launch(float* V, int64_t ldv, int64_t d, int kc, int r, hipStream_t stream);
 // evals[0..k) -= shift (device).
 int unshift_launch(float* evals, int k, double shift, hipStream_t stream);
+// evals[j] = v_j^T S v_j / v_j^T v_j in double for the k columns of V (S: stype).
+size_t rq_workspace_bytes(int64_t d);
+int rq_launch(const void* S, int stype, int64_t d, int64_t lds, const float* V, int64_t ldv, int k,
+              float* evals, void* ws, hipStream_t stream);
 
 // Oja (oja.hip).
 size_t oja_workspace_bytes(int64_t b, int64_t d, int k);

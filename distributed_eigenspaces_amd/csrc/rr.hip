@@ -20,6 +20,8 @@
 //    columns with g ~ 0 - null directions of A - keep Q w_j);
 //    the top-k Ritz vectors are written to V (column-major, ascending order).
 //  rr_finish_kernel: relative residuals, eigenvalues (ascending) and their max.
+#include <algorithm>
+
 #include "deig_internal.hpp"
 
 namespace deig {
@@ -671,6 +673,74 @@ __global__ void unshift_kernel(float* __restrict__ evals, int k, double shift) {
   if (j < k) evals[j] = (float)((double)evals[j] - shift);
 }
 
+// Final eigenvalues as Rayleigh quotients in DOUBLE: lam_j = v_j^T S v_j / v_j^T v_j
+// from the explicit S (float or double, row-major lds) and the returned vectors.
+// The fp32 Rayleigh-Ritz values carry ~1e-7 of the operator's scale (a few ulps of
+// |H| in the small solve); a quotient of a vector with sin(angle) ~ 1e-6 is exact to
+// ~1e-12 of the spread, and it is taken on S itself - unshifted, undeflated.
+// grid (cdiv(d, RQ_R), vector groups of RQ_K); thread = (row tid / 8, 4 vectors).
+constexpr int RQ_R = 32, RQ_L = 64, RQ_K = 32, RQ_GY = 4;
+template <typename T>
+__global__ __launch_bounds__(256) void rq_kernel(const T* __restrict__ S, int64_t lds, int64_t d,
+                                                 const float* __restrict__ V, int64_t ldv, int j0,
+                                                 int k, double* __restrict__ part) {
+  __shared__ double Ss[RQ_R][RQ_L + 1];
+  __shared__ double Vs[RQ_L][RQ_K];
+  __shared__ double red[RQ_R][2 * RQ_K + 1];
+  const int tid = threadIdx.x, i = tid >> 3, jg = tid & 7;
+  const int64_t r0 = (int64_t)blockIdx.x * RQ_R;
+  const int jb = j0 + blockIdx.y * RQ_K;  // first vector of this block
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t l0 = 0; l0 < d; l0 += RQ_L) {
+    for (int e = tid; e < RQ_R * RQ_L; e += 256) {
+      const int rr = e / RQ_L, cc = e - rr * RQ_L;
+      const int64_t row = r0 + rr, col = l0 + cc;
+      Ss[rr][cc] = (row < d && col < d) ? (double)S[row * lds + col] : 0.0;
+    }
+    for (int e = tid; e < RQ_L * RQ_K; e += 256) {
+      const int jj = e / RQ_L, ll = e - jj * RQ_L;
+      const int64_t l = l0 + ll;
+      Vs[ll][jj] = (l < d && jb + jj < k) ? (double)V[(int64_t)(jb + jj) * ldv + l] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int ll = 0; ll < RQ_L; ++ll) {
+      const double s = Ss[i][ll];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = fma(s, Vs[ll][4 * jg + u], acc[u]);
+    }
+    __syncthreads();
+  }
+  const int64_t row = r0 + i;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int j = jb + 4 * jg + u;
+    const double v = (row < d && j < k) ? (double)V[(int64_t)j * ldv + row] : 0.0;
+    red[i][4 * jg + u] = v * acc[u];
+    red[i][RQ_K + 4 * jg + u] = v * v;
+  }
+  __syncthreads();
+  if (tid < 2 * RQ_K) {
+    double s = 0.0;
+    for (int rr = 0; rr < RQ_R; ++rr) s += red[rr][tid];  // fixed order
+    part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 2 * RQ_K + tid] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void rq_finish_kernel(const double* __restrict__ part, int nbx,
+                                                        int j0, int k, float* __restrict__ evals) {
+  const int t = blockIdx.x * 256 + threadIdx.x;  // vector j0 + t
+  if (t >= RQ_GY * RQ_K || j0 + t >= k) return;
+  const int gy = t / RQ_K, jj = t - gy * RQ_K;
+  double q = 0.0, nn = 0.0;
+  for (int b = 0; b < nbx; ++b) {
+    const double* p = part + ((int64_t)gy * nbx + b) * 2 * RQ_K;
+    q += p[jj];
+    nn += p[RQ_K + jj];
+  }
+  if (nn > 0.0) evals[j0 + t] = (float)(q / nn);
+}
+
 size_t rr_small_shm(int p) {
   return (size_t)(2 * p * p + 7 * p + RT / 64 + 20) * sizeof(float);
 }
@@ -723,6 +793,30 @@ int deflate_orth_launch(float* V, int64_t ldv, int64_t d, int kc, int r, hipStre
   DEIG_REQUIRE(r >= 1 && kc >= 1, "deflate_orth: r=%d kc=%d out of range", r, kc);
   hipLaunchKernelGGL(deflate_orth_kernel, dim3(kc), dim3(256), 0, stream, V, ldv, d, kc, r);
   DEIG_HIP_CHECK(hipGetLastError());
+  return DEIG_OK;
+}
+
+size_t rq_workspace_bytes(int64_t d) {
+  return (size_t)cdiv(d, RQ_R) * RQ_GY * 2 * RQ_K * sizeof(double);
+}
+
+int rq_launch(const void* S, int stype, int64_t d, int64_t lds, const float* V, int64_t ldv, int k,
+              float* evals, void* ws, hipStream_t stream) {
+  double* part = static_cast<double*>(ws);
+  const int nbx = (int)cdiv(d, RQ_R);
+  for (int j0 = 0; j0 < k; j0 += RQ_GY * RQ_K) {
+    const int gy = (int)std::min<int64_t>(RQ_GY, cdiv(k - j0, RQ_K));
+    const dim3 grid((unsigned)nbx, (unsigned)gy);
+    if (stype == DEIG_F64)
+      hipLaunchKernelGGL(rq_kernel<double>, grid, dim3(256), 0, stream,
+                         static_cast<const double*>(S), lds, d, V, ldv, j0, k, part);
+    else
+      hipLaunchKernelGGL(rq_kernel<float>, grid, dim3(256), 0, stream,
+                         static_cast<const float*>(S), lds, d, V, ldv, j0, k, part);
+    DEIG_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(rq_finish_kernel, dim3(1), dim3(256), 0, stream, part, nbx, j0, k, evals);
+    DEIG_HIP_CHECK(hipGetLastError());
+  }
   return DEIG_OK;
 }
 

@@ -580,13 +580,13 @@ __device__ __forceinline__ void segment(const SSched& s, unsigned char* lds, int
 //   WAR: every L part retires its reads (lgkmcnt(0)) before its closing barrier, and
 //   a buffer is restaged from the next K-tile's L_0 on - after the lagging group's
 //   last read of it (its L_{P-1} of the K-tile before) has passed that barrier.
-template <int P>
+template <int P, int QD, int PRIO>
 __device__ __forceinline__ void segment_st(const SSched& s, unsigned char* lds, int tile,
                                            int64_t k0, int64_t k1, int slot, bool partial,
                                            int pace_j) {
-  static_assert(P == 2 || P == 4, "phases per K-tile");
-  constexpr int MBP = 8 / P;              // A blocks (16 rows) per phase
-  constexpr int QD = P == 2 ? 1 : 2;      // phases that issue the next K-tile's pieces
+  static_assert(P == 2 || P == 4 || P == 8, "phases per K-tile");
+  static_assert(QD >= 1 && QD < P, "the next K-tile's pieces go out before its last phase");
+  constexpr int MBP = 8 / P;  // A blocks (16 rows) per phase
   constexpr int BUF_B = Geo<2>::BUF_B;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -627,7 +627,7 @@ __device__ __forceinline__ void segment_st(const SSched& s, unsigned char* lds, 
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (i < u0 / 2 || i >= u1 / 2) continue;
+        if (2 * i < u0 || 2 * i >= u1) continue;
         const int idx = wave * 4 + i;
         const int sl = idx >> 2, p = idx & 3;
         dma16(rsrc, l16 + i0 / BT * BLOCK_B + sl * SLICE_B + p * 1024, buf + sl * SLICE_B + p * 1024);
@@ -670,7 +670,8 @@ __device__ __forceinline__ void segment_st(const SSched& s, unsigned char* lds, 
           }
           ++since;
         }
-        if (more && q < QD) stage_part(k0 + t + 1, nxt, q * (8 / QD), (q + 1) * (8 / QD));
+        // the next K-tile's 8 pieces over phases 0 .. QD-1 (QD = 3: 3, 3, 2)
+        if (more && q < QD) stage_part(k0 + t + 1, nxt, (8 * q + QD - 1) / QD, (8 * (q + 1) + QD - 1) / QD);
         if (q == 0) {
 #pragma unroll
           for (int nb = 0; nb < 4; ++nb) {
@@ -689,6 +690,7 @@ __device__ __forceinline__ void segment_st(const SSched& s, unsigned char* lds, 
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         bar();
         // ---------------- M part
+        if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int m = 0; m < MBP; ++m) {
           const int mb = q * MBP + m;
@@ -702,6 +704,7 @@ __device__ __forceinline__ void segment_st(const SSched& s, unsigned char* lds, 
           for (int nb = 0; nb < 4; ++nb)
             acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[m], bhi[nb], acc.a[mb][nb], 0, 0, 0);
         }
+        if (PRIO) __builtin_amdgcn_s_setprio(0);
         bar();
       }
     }
@@ -721,7 +724,7 @@ __device__ __forceinline__ void segment_st(const SSched& s, unsigned char* lds, 
   }
 }
 
-template <int P>
+template <int P, int QD, int PRIO>
 __global__ __launch_bounds__(NTHR) void syrks_st_kernel(SSched s) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[2 * Geo<2>::BUF_B];
   const int L = xcd_logical(blockIdx.x, s.G);
@@ -744,7 +747,7 @@ __global__ __launch_bounds__(NTHR) void syrks_st_kernel(SSched s) {
       k1 = __builtin_amdgcn_readfirstlane((int)(s.NK * (sg + 1) / s.nseg));
     }
     const int pace_j = (!partial && s.pace_kt > 0) ? (int)(w * (s.NK / s.pace_kt)) : -1;
-    segment_st<P>(s, lds, tile, k0, k1, slot, partial, pace_j);
+    segment_st<P, QD, PRIO>(s, lds, tile, k0, k1, slot, partial, pace_j);
   }
 }
 
@@ -956,13 +959,35 @@ int64_t default_chunk_rows(int64_t n, int64_t d) {
 // process, profiles/r02l_syrk_fused_ab.log): d = 3072 (config 2) fused 27.3 ms vs
 // 29.0 ms; d = 8192 (config 3 shard) fused 370 ms vs 336 ms.
 // A/B builds (tools/, never the shipped library) fix one with -DDEIG_AB_SYRK_VARIANT=N.
+// Staggered-phase variants are 1PQR0: P phases per K-tile, the next K-tile's
+// pieces over Q of them, R = 1: s_setprio(1) around the MFMA clusters.
+#ifdef DEIG_AB_SYRK_VARIANT
+constexpr int kSyrkLarge = DEIG_AB_SYRK_VARIANT;
+#else
+constexpr int kSyrkLarge = 14200;
+#endif
 int syrk_variant(int64_t d) {
 #ifdef DEIG_AB_SYRK_VARIANT
   (void)d;
   return DEIG_AB_SYRK_VARIANT;
 #else
-  return d <= 4096 ? 163 : 162;
+  return d <= 4096 ? 163 : kSyrkLarge;
 #endif
+}
+
+// The split-pass kernel of variant V (instantiated for kSyrkLarge only).
+template <int V>
+void launch_split_pass_kernel(int G, hipStream_t stream, const SSched& s) {
+  if constexpr (V >= 10000) {
+    hipLaunchKernelGGL((syrks_st_kernel<(V / 1000) % 10, (V / 100) % 10, (V / 10) % 10>), dim3(G),
+                       dim3(NTHR), 0, stream, s);
+  } else if constexpr (V == 13 || V == 14 || V == 15) {
+    hipLaunchKernelGGL((syrks_kernel<32, 1, V - 10, false>), dim3(G), dim3(NTHR), 0, stream, s);
+  } else if constexpr (V == 22) {
+    hipLaunchKernelGGL((syrks_kernel<32, 2, 2, false>), dim3(G), dim3(NTHR), 0, stream, s);
+  } else {
+    hipLaunchKernelGGL((syrks_kernel<16, 2, 2, false>), dim3(G), dim3(NTHR), 0, stream, s);
+  }
 }
 
 }  // namespace
@@ -974,7 +999,7 @@ size_t syrk_split_workspace_bytes(int64_t n, int64_t d) {
 }
 
 int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha, float* S,
-                      int64_t lds, void* ws, size_t ws_bytes, hipStream_t stream) {
+                      int64_t lds, void* ws, size_t ws_bytes, hipStream_t stream, bool accumulate) {
   DEIG_REQUIRE(n >= 1, "syrk: n must be >= 1 (got %lld)", (long long)n);
   DEIG_REQUIRE(d >= 1 && d % 4 == 0, "syrk: d must be a positive multiple of 4 (got %lld)",
                (long long)d);
@@ -1049,7 +1074,7 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
     DEIG_HIP_CHECK(hipMemsetAsync(corr, 0, sizeof(float) * (size_t)(yb * L.dp), stream));
     s.NK = cdiv(n, ROWS_PAD);
     s.nseg = (int)L.nseg;
-    s.beta = 0;
+    s.beta = accumulate ? 1 : 0;
     s.flush_kt = (int)(flush_rows / ROWS_PAD);
     if (s.flush_kt < 1) s.flush_kt = 1;
     if (s.pace_kt > 0) DEIG_HIP_CHECK(hipMemsetAsync(s.pace, 0, 8 * 128, stream));
@@ -1077,19 +1102,11 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
     DEIG_HIP_CHECK(hipGetLastError());
     s.NK = nk;
     s.nseg = (int)L.nseg;
-    s.beta = c > 0 ? 1 : 0;
+    s.beta = (c > 0 || accumulate) ? 1 : 0;
     s.flush_kt = (int)(flush_rows / (16 * kt_steps));
-    const bool mf16 = variant >= 100;
+    const bool mf16 = variant >= 100;  // 162, 163, 1PQR0: 16x16x32 slabs
     if (s.pace_kt > 0) DEIG_HIP_CHECK(hipMemsetAsync(s.pace, 0, 8 * 128, stream));
-    switch (variant) {
-      case 172: hipLaunchKernelGGL(syrks_st_kernel<2>, dim3(G), dim3(NTHR), 0, stream, s); break;
-      case 174: hipLaunchKernelGGL(syrks_st_kernel<4>, dim3(G), dim3(NTHR), 0, stream, s); break;
-      case 13: hipLaunchKernelGGL((syrks_kernel<32, 1, 3, false>), dim3(G), dim3(NTHR), 0, stream, s); break;
-      case 14: hipLaunchKernelGGL((syrks_kernel<32, 1, 4, false>), dim3(G), dim3(NTHR), 0, stream, s); break;
-      case 15: hipLaunchKernelGGL((syrks_kernel<32, 1, 5, false>), dim3(G), dim3(NTHR), 0, stream, s); break;
-      case 22: hipLaunchKernelGGL((syrks_kernel<32, 2, 2, false>), dim3(G), dim3(NTHR), 0, stream, s); break;
-      default: hipLaunchKernelGGL((syrks_kernel<16, 2, 2, false>), dim3(G), dim3(NTHR), 0, stream, s); break;
-    }
+    if (variant != 163) launch_split_pass_kernel<kSyrkLarge == 163 ? 162 : kSyrkLarge>(G, stream, s);
     DEIG_HIP_CHECK(hipGetLastError());
     if (s.R > 0) {
       if (mf16)

@@ -111,7 +111,8 @@ def default_subspace(d: int, k: int) -> int:
 # ---------------------------------------------------------------- covariance
 def sigma_hat(x: torch.Tensor, alpha: float | None = None,
               out: torch.Tensor | None = None, algo: str = "auto",
-              shift: bool | None = None, dtype: torch.dtype | None = None) -> torch.Tensor:
+              shift: bool | None = None, dtype: torch.dtype | None = None,
+              accumulate: bool = False) -> torch.Tensor:
     """Sigma_hat = alpha * X^T X with alpha = 1/n by default (uncentered).
 
     GPU replacement for ``SlaveNode.compute_sigma_hat_`` (distributed.py:59-70).
@@ -127,6 +128,8 @@ def sigma_hat(x: torch.Tensor, alpha: float | None = None,
       * uint8 samples: the exact integer path (sigma_hat_u8; 2-D raw bytes or
         N x H x W x 3 pixels with the reference's grayscale fused in).
     dtype: result dtype (float32 / float64) for the shifted and uint8 paths.
+    accumulate: ``out += alpha X^T X`` (float32 split3 path; a covariance streamed
+    through in row blocks, DEIG_SYRK_ACCUMULATE).
     """
     if not isinstance(x, torch.Tensor):
         x = torch.as_tensor(x)
@@ -135,11 +138,18 @@ def sigma_hat(x: torch.Tensor, alpha: float | None = None,
     if shift is None:
         shift = x.dtype == torch.float64
     if shift:
+        if accumulate:
+            raise ValueError("accumulate is for the float32 split3 path (shift=False)")
         return sigma_hat_shift(x, alpha=alpha, out=out, dtype=dtype or torch.float64)
     if algo not in _lib.SYRK_ALGOS:
         raise ValueError(f"algo must be one of {sorted(_lib.SYRK_ALGOS)}, got {algo!r}")
     code = _lib.SYRK_ALGOS[algo]
     x = require_device_tensor(x, "sigma_hat")
+    if accumulate:
+        if out is None or algo == "fp32" or x.shape[1] % 4 or not out.is_contiguous():
+            raise ValueError("accumulate needs out (contiguous d x d float32), d % 4 == 0 and "
+                             "the split3 algorithm")
+        code = _lib.DEIG_SYRK_SPLIT3 | _lib.DEIG_SYRK_ACCUMULATE
     if x.dim() != 2:
         raise ValueError(f"x must be 2-D (n, d), got {tuple(x.shape)}")
     n, d = x.shape

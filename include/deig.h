@@ -59,6 +59,9 @@ const char* deig_last_error(void);
 #define DEIG_SYRK_FP32 2
 #define DEIG_SYRK_DEFAULT DEIG_SYRK_AUTO
 #define DEIG_SYRK_SPLIT_MIN_ROWS 1024
+/* OR-ed into the algorithm of deig_syrk_f32_ex (SPLIT3 only): S += alpha X^T X -
+ * one covariance streamed through in row blocks (e.g. a shard larger than HBM). */
+#define DEIG_SYRK_ACCUMULATE 0x100
 
 /* Sigma_hat = alpha * X^T X  (alpha = 1/n reproduces the reference).
  * Replaces SlaveNode.compute_sigma_hat_  distributed.py:59-70

@@ -22,10 +22,32 @@ def lib_path(v):
 
 
 def build(variants):
+    """Only syrk_split.hip differs between variants: compile it per variant (in
+    parallel) and link it with the main build's other objects."""
+    import subprocess
+
     from distributed_eigenspaces_amd import _build
     os.makedirs(LIBDIR, exist_ok=True)
+    _build.build_library()  # the main objects are current
+    objdir = os.path.join(_build.HERE, "build")
+    hipcc = _build._hipcc()
+    flags = [f"--offload-arch={_build.ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+             "-Wno-unused-function", "-Wno-inline-asm"] + _build.EXTRA_FLAGS["syrk_split.hip"]
+    procs = []
     for v in variants:
-        _build.build_library(force=True, defines=[f"-DDEIG_AB_SYRK_VARIANT={v}"], out=lib_path(v))
+        obj = os.path.join(LIBDIR, f"syrk_split_v{v}.o")
+        cmd = [hipcc] + flags + [f"-DDEIG_AB_SYRK_VARIANT={v}", "-c",
+                                 os.path.join(_build.CSRC, "syrk_split.hip"), "-o", obj]
+        procs.append((v, obj, subprocess.Popen(cmd)))
+    for v, obj, p in procs:
+        if p.wait() != 0:
+            raise RuntimeError(f"variant {v} failed to compile")
+        others = [os.path.join(objdir, s.replace(".hip", ".o")) for s in _build.SOURCES
+                  if s != "syrk_split.hip"]
+        subprocess.run([hipcc, f"--offload-arch={_build.ARCH}", "-shared", "-fPIC", "-o", lib_path(v),
+                        obj] + others, check=True)
+        os.remove(obj)
+        print("built", lib_path(v), flush=True)
 
 
 def run(variants, n, d, rounds, reps):
