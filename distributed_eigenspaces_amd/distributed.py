@@ -307,8 +307,8 @@ def load_dataset(path):
 
     A CIFAR batch directory (load_data.py:18-33) stays uint8 (N, 32, 32, 3): the
     grayscale + flatten of :170-173 is fused into the exact integer covariance on
-    the GPU (linalg.sigma_hat_u8), which gives the correctly rounded value of the
-    reference's float64 result.  A ``.npy`` file (addition, for non-CIFAR data and
+    the GPU (linalg.sigma_hat_u8), which gives the reference's float64 result within
+    one fp32 ulp (float64 output: to double rounding).  A ``.npy`` file (addition, for non-CIFAR data and
     tests) is used as stored (loaded without pickle); a 4-D float array there gets
     the reference's host preprocessing."""
     import os

@@ -233,8 +233,8 @@ def sigma_hat_u8(x: torch.Tensor, mode: str = "auto", alpha: float | None = None
         distributed.py:170-173 - fused into the covariance; or (n, 3m) rows with
         mode "gray" explicitly.
     Returns alpha * V^T V (alpha = 1/n: distributed.py:59-70) as a (d, d) tensor of
-    ``dtype`` (float32: the correctly rounded value of the exact result; float64:
-    exact to double rounding).  Every product and sum is an integer computation
+    ``dtype`` (float32: within one ulp of the exact result - a double quotient
+    rounded to float; float64: exact to double rounding).  Every product and sum is an integer computation
     (include/deig.h deig_syrk_u8), so there is no accumulation error at all.
     """
     if not isinstance(x, torch.Tensor):

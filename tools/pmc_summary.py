@@ -5,7 +5,7 @@ import glob
 import sys
 
 out = sys.argv[1]
-kern = sys.argv[2] if len(sys.argv) > 2 else "syrks_kernel"
+kern = sys.argv[2] if len(sys.argv) > 2 else "syrks_q_kernel"
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in glob.glob(f"{out}/*/p_counter_collection.csv"):
     for r in csv.DictReader(open(f)):

@@ -16,7 +16,7 @@ timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o p -- \
   python3 $R/tools/run_syrk_once.py > $OUT/write.log 2>&1 || { echo "write pass failed"; tail $OUT/write.log; exit 1; }
 python3 $R/tools/pmc_traffic.py $OUT/fetch $OUT/write $OUT/pmc_syrk_c3_split3.json 2097152 8192 \
-  "covariance split3 (split_kernel + syrks_kernel + syrks_reduce_kernel + diag_corr_kernel)" > /dev/null \
+  "covariance split3 (split_kernel + syrks_q_kernel + syrks_reduce_kernel + diag_corr_kernel)" > /dev/null \
   && python3 - $OUT/pmc_syrk_c3_split3.json $TAG <<'PY'
 import json, sys, time
 p, tag = sys.argv[1:3]

@@ -5,6 +5,7 @@ shipped library has no knobs).
 
   python tools/syrk_ab.py build 162 174            # here (CPU): tools/ab_libs/libdeig_v*.so
   python tools/syrk_ab.py run 162 174 [--n N --d D --rounds R]   # on the GPU box
+  python tools/syrk_ab.py check 162 174 --n 131071 --d 8192       # vs float64, poisoned workspace
 """
 import argparse
 import ctypes
@@ -101,9 +102,47 @@ def run(variants, n, d, rounds, reps):
               flush=True)
 
 
+def check(variants, n, d):
+    """Each variant on a NaN-poisoned workspace (every byte 0xff) vs float64, at a
+    ragged n: a variant that leaves any part of its image unwritten reads NaN."""
+    import torch
+
+    from distributed_eigenspaces_amd import _lib, synthetic
+    dev = torch.device("cuda", 0)
+    U = synthetic.planted_basis(d, 64, seed=0, device=dev)
+    X = synthetic.spiked_samples(n, U, seed=1)
+    Xd = X.double()
+    ref = (Xd.t() @ Xd) / n
+    del Xd
+    scale = ref.abs().max().item()
+    dref = torch.diagonal(ref)
+    for v in variants:
+        L = ctypes.CDLL(lib_path(v))
+        for name in ("deig_syrk_f32_ex", "deig_syrk_workspace_ex", "deig_last_error"):
+            res, args = _lib.SIGNATURES[name]
+            getattr(L, name).restype = res
+            getattr(L, name).argtypes = args
+        nbytes = L.deig_syrk_workspace_ex(n, d, _lib.DEIG_SYRK_SPLIT3)
+        ws = torch.full((nbytes,), 255, dtype=torch.uint8, device=dev)
+        S = torch.full((d, d), float("nan"), dtype=torch.float32, device=dev)
+        st = torch.cuda.current_stream(dev)
+        for rep in range(2):
+            rc = L.deig_syrk_f32_ex(X.data_ptr(), n, d, d, ctypes.c_float(1.0 / n), S.data_ptr(), d,
+                                    _lib.DEIG_SYRK_SPLIT3, ws.data_ptr(), nbytes, st.cuda_stream)
+            if rc:
+                raise RuntimeError(f"v{v}: {L.deig_last_error()}")
+            torch.cuda.synchronize()
+            err = ((S.double() - ref).abs().max().item()) / scale
+            derr = ((torch.diagonal(S).double() - dref).abs().max().item()) / scale
+            print(f"check v{v} n={n} d={d} launch {rep}: max|S - S64|/max|S64| = {err:.3e} "
+                  f"(diagonal {derr:.3e}); finite {bool(torch.isfinite(S).all())}; "
+                  f"symmetric {bool(torch.equal(S, S.t()))}", flush=True)
+        del ws, S
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("cmd", choices=["build", "run"])
+    ap.add_argument("cmd", choices=["build", "run", "check"])
     ap.add_argument("variants", nargs="+", type=int)
     ap.add_argument("--n", type=int, default=1 << 21)
     ap.add_argument("--d", type=int, default=8192)
@@ -112,6 +151,8 @@ def main():
     a = ap.parse_args()
     if a.cmd == "build":
         build(a.variants)
+    elif a.cmd == "check":
+        check(a.variants, a.n, a.d)
     else:
         run(a.variants, a.n, a.d, a.rounds, a.reps)
 
