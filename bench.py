@@ -450,9 +450,13 @@ def run_oneshot(args, cfg, world, rank, dev):
     # my_threading.Slave thread on its own HIP stream, started as soon as its
     # covariance is enqueued, so the latency-bound parts of one solve (the
     # single-workgroup Rayleigh-Ritz step, host syncs) overlap the others' sweeps.
-    concurrent = W > 1 and not args.serial_workers
+    concurrent = W > 1 and not args.serial_workers and args.threaded_workers
+    # default for W > 1: the W covariances back to back, then ONE batched solve
+    # (linalg.topk_eigh_batch: each worker's sweeps on its own stream, the small
+    # Rayleigh-Ritz solves of all W workers in one launch per step)
+    batched = W > 1 and not args.serial_workers and not args.threaded_workers
     Ss = [S] + [torch.empty((d, d), dtype=torch.float32, device=dev)
-                for _ in range(W - 1)] if concurrent else None
+                for _ in range(W - 1)] if (concurrent or batched) else None
     side = [torch.cuda.Stream(dev) for _ in range(W)] if concurrent else None
     torch.cuda.synchronize()
     m = world * W
@@ -503,7 +507,38 @@ def run_oneshot(args, cfg, world, rank, dev):
             rec["server"].append(t3 - t2)
         return rs[-1], res
 
+    def step_batched(record: bool):
+        t0 = time.perf_counter()
+        evs = []
+        for w in range(W):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            e[0].record(stream)
+            de.sigma_hat(X[w * ni:(w + 1) * ni], out=Ss[w], algo=args.syrk_algo)
+            e[1].record(stream)
+            evs.append(e)
+        rs = de.topk_eigh_batch(Ss, k, check_finite=False)
+        for w, r in enumerate(rs):
+            Wt_local[w * k:(w + 1) * k].copy_(r.V.t())
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        Wt = gather_bases(Wt_local)
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        res = None
+        if rank == 0:
+            res = de.projavg_topk(Wt, k, 1.0 / m, q0=Wt[:k].t())
+        torch.cuda.synchronize(dev)
+        t3 = time.perf_counter()
+        if record:
+            syrk_ev.extend((e, r.sweeps) for e, r in zip(evs, rs))
+            rec["worker"].append(t1 - t0)
+            rec["gather"].append(t2 - t1)
+            rec["server"].append(t3 - t2)
+        return rs[-1], res
+
     def step(record: bool):
+        if batched:
+            return step_batched(record)
         if concurrent:
             return step_concurrent(record)
         t0 = time.perf_counter()
@@ -644,7 +679,9 @@ def run_oneshot(args, cfg, world, rank, dev):
     line = base_line(args, world, elapsed, float(n) * world * args.steps, "u8" if u8 else "f32", {
         "workload": cfg["label"], "rows_per_gpu": n, "total_rows": n * world, "d": d, "k": k,
         "workers_per_gpu": W, "rows_per_worker": ni, "workers_total": m, "subspace_p": p,
-        "parallelism": f"dp{world} ({W} logical worker(s) per GPU, RCCL all-gather of bases)"})
+        "parallelism": f"dp{world} ({W} logical worker(s) per GPU, RCCL all-gather of bases)",
+        "worker_solves": ("batched (deig_topk_sym_batch)" if batched else
+                          "my_threading.Slave threads" if concurrent else "serial")})
     if u8:
         line["data"] = ("synthetic spiked bytes: clip(round(128 + 20 x)) of spiked rows (planted "
                         "U, theta 8->4)" + ("; 3 channels with independent noise" if u8 == "gray"
@@ -744,8 +781,9 @@ def run_oja(args, cfg, world, rank, dev):
         "rows_per_gpu_per_step": agg * b,
         "parallelism": f"dp{world} (one Oja stream per GPU; RCCL all-gather + broadcast of "
                        f"bases every {agg} batches)"})
-    line["roofline"] = {"bound": "hbm", "kernel": "Oja steps (skinny NN Xb*V + skinny TN Xb^T*T "
-                        "+ CholQR2 every 8 batches), whole op per batch",
+    line["roofline"] = {"bound": "hbm", "kernel": "Oja steps (oja_nn_kernel Xb*V + oja_tn_kernel "
+                        "V += c Xb^T*T, bf16x3 split products; CholQR every 8 batches), whole op "
+                        "per batch",
                         "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK, "traffic": None,
                         "algorithmic": f"8*b*d = {byt:.4e} bytes per batch (Xb read twice)",
@@ -773,7 +811,10 @@ def main():
                     help="c3: skip streaming all 2^24 rows through one GPU (time_to_eigenspace)")
     ap.add_argument("--serial-workers", action="store_true",
                     help="W > 1 workers per GPU: run each worker's solve after its covariance on "
-                         "one stream (default: solves in Slave threads on their own streams)")
+                         "one stream (default: one batched solve, deig_topk_sym_batch)")
+    ap.add_argument("--threaded-workers", action="store_true",
+                    help="W > 1: each worker's solve in a my_threading.Slave thread on its own "
+                         "stream (the r02 mode)")
     ap.add_argument("--syrk-algo", default="auto", choices=["auto", "split3", "fp32"])
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = rehearsal of the N>1 control flow with ranks sharing one GPU")

@@ -14,6 +14,6 @@ Drop-in modules: ``distributed`` (Node / SlaveNode / MasterNode / run_* / main),
 compute_segma_hat, online loop).
 """
 from .linalg import (EigResult, default_subspace, oja_step, oja_steps, projavg_topk,  # noqa: F401
-                     sigma_hat, stack_bases, sym_apply, sym_power, topk_eigh)
+                     sigma_hat, stack_bases, sym_apply, sym_power, topk_eigh, topk_eigh_batch)
 
 __version__ = "0.1.0"

@@ -10,6 +10,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
+#include <vector>
 
 #include "deig_internal.hpp"
 
@@ -319,179 +323,220 @@ struct Solver {
   hipStream_t st;
   float lam_h[kMaxP];
   float res_h[kMaxP + 1];  // per-column residuals of the last RR (descending Ritz order)
+  int jconv_h = 1;         // the last RR's Jacobi converged (rr.hip info[3])
   int it = 0;              // sweeps done (all blocks and restarts)
   float last = 3.4e38f;
   bool converged = false;
+  // the iteration in progress (iter_begin .. a cycle_finish that ends it)
+  int kc = 0, pb = 0;
+  float* Vb = nullptr;
+  int64_t ldv = 0;
+  float* evb = nullptr;
+  bool allow_early = false, early = false;
+  int rr_every = 4, jcap_sweeps = 2, jcap = 30, nrr = 0, start = 0, since_best = 0;
+  float tau = 0.f, jcap_above = 1e-4f, best = 3.4e38f;
+  bool fuse = false;
+  int ncheb_dbg = 0;
 
   // Pairs a block's dominant-pair deflation would lock (0: none).
-  int dominant(int kc) const {
-    if (!(lam_h[kc - 1] > 0.f && lam_h[0] >= kDeflateRatio * lam_h[kc - 1])) return 0;
+  int dominant(int kc_) const {
+    if (!(lam_h[kc_ - 1] > 0.f && lam_h[0] >= kDeflateRatio * lam_h[kc_ - 1])) return 0;
     int r = 0;
-    while (r < kc - 1 && r < kMaxDeflate && lam_h[r] >= kDeflateRatio * lam_h[kc - 1]) ++r;
+    while (r < kc_ - 1 && r < kMaxDeflate && lam_h[r] >= kDeflateRatio * lam_h[kc_ - 1]) ++r;
     return r;
   }
 
   // Subspace iteration for the top kc pairs of the current operator on a pb-column
-  // basis (initialised by the caller); the pairs go to Vb / evb (ascending).  early
-  // (optional): stop as soon as the dominant pairs are converged (*early_out).
-  int iterate(int kc, int pb, float* Vb, int64_t ldv, float* evb, bool allow_early,
-              bool* early_out) {
-    // Cycles: [filter / power sweeps] + one sweep with a Rayleigh-Ritz step (Gram +
-    // small solve + update + residual check).  Between two RRs either a Chebyshev
-    // filter of planned degree runs (cheb_plan) or, while the residual is above
-    // cheb_above, rr_every - 1 plain power steps Q <- A Q on the Ritz vectors of the
-    // last RR (same span as subspace iteration; the generalised RR copes with the
-    // non-orthonormal basis).  The single-workgroup small solve is the latency-bound
-    // part of a cycle, so spacing RRs divides its cost.  Power steps: every 4th sweep
-    // is an RR when the basis has >= 16 guard columns beyond k (measured: d=8192
-    // k=64 p=80 6.2 vs 9.0 ms, d=3072 k=16 p=32 1.4 vs 1.9 ms); every 2nd without
-    // them (d=16384 k=128 p=128: 23 sweeps / 47 ms vs 41 / 54 ms).
-    const int rr_every = o.rr_every > 0 ? o.rr_every : (pb - kc >= 16 ? 4 : 2);
-    const float tau = rr_every > 1 ? powf(0.1f, 1.0f / (float)(rr_every - 1)) : 0.f;
+  // basis (initialised by the caller); the pairs go to Vb / evb (ascending).
+  // allow_early: stop as soon as the dominant pairs are converged (early).
+  //   A cycle = [filter / power sweeps] + one sweep with a Rayleigh-Ritz step (Gram +
+  // small solve + update + residual check): cycle_sweeps (through the Gram),
+  // cycle_rr_small, cycle_update (+ the residual copies), a stream sync, then
+  // cycle_finish.  The batched driver (solve_batch) runs the small solves of several
+  // problems in one launch between cycle_sweeps and cycle_update.
+  //   Between two RRs either a Chebyshev filter of planned degree runs (cheb_plan)
+  // or, while the residual is above cheb_above, rr_every - 1 plain power steps
+  // Q <- A Q on the Ritz vectors of the last RR (same span as subspace iteration;
+  // the generalised RR copes with the non-orthonormal basis).  The single-workgroup
+  // small solve is the latency-bound part of a cycle, so spacing RRs divides its
+  // cost.  Power steps: every 4th sweep is an RR when the basis has >= 16 guard
+  // columns beyond k (measured: d=8192 k=64 p=80 6.2 vs 9.0 ms, d=3072 k=16 p=32 1.4
+  // vs 1.9 ms); every 2nd without them (d=16384 k=128 p=128: 23 sweeps / 47 ms vs
+  // 41 / 54 ms).
+  void iter_begin(int kc_, int pb_, float* Vb_, int64_t ldv_, float* evb_, bool allow_early_) {
+    kc = kc_;
+    pb = pb_;
+    Vb = Vb_;
+    ldv = ldv_;
+    evb = evb_;
+    allow_early = allow_early_;
+    early = false;
+    rr_every = o.rr_every > 0 ? o.rr_every : (pb - kc >= 16 ? 4 : 2);
+    tau = rr_every > 1 ? powf(0.1f, 1.0f / (float)(rr_every - 1)) : 0.f;
     // Early Rayleigh-Ritz steps run a capped Jacobi: worker solves (explicit S) 2
     // sweeps while the residual is above 1e-4 (r02s A/B, profiles/r02s_jacobi_cap_ab.log:
     // c1 +8 %, c1g +14 % over 3 above 1e-2, c3 the same time in 16 sweeps instead of
     // 12; 1 sweep fails the bars); the server's implicit projector average
     // (eigenvalues clustered near 1) 3 above 1e-2 (the tighter cap cost config 4's
     // aggregation 2.05 -> 2.65 ms).
-    const int jcap_sweeps = o.jcap_sweeps >= 0 ? o.jcap_sweeps : (op.implicit ? 3 : 2);
-    const float jcap_above = o.jcap_above >= 0.f ? o.jcap_above : (op.implicit ? 1e-2f : 1e-4f);
-    const bool fuse = w.sweep_ws != nullptr;
-    float best = 3.4e38f;
-    int since_best = 0, nrr = 0, start = it;
+    jcap_sweeps = o.jcap_sweeps >= 0 ? o.jcap_sweeps : (op.implicit ? 3 : 2);
+    jcap_above = o.jcap_above >= 0.f ? o.jcap_above : (op.implicit ? 1e-2f : 1e-4f);
+    fuse = w.sweep_ws != nullptr;
+    best = 3.4e38f;
+    since_best = 0;
+    nrr = 0;
+    start = it;
     last = 3.4e38f;
     converged = false;
-    while (it - start < max_sweeps) {
-      const int budget = max_sweeps - (it - start);
-      // Sweep precision by residual: early sweeps (above fast_until) take S as its
-      // two leading bf16 pieces too - three products, no split in the sweep, ~2^-16
-      // relative, 100x below the residual there (sweep.hip sweep_products SP = 2);
-      // then Q rounded to two pieces (five products) down to round_until; the
-      // closing sweeps exact (the rounding puts ~4e-6 relative noise into the basis
-      // each sweep: a floor under the residual).
-      const int smode = (o.fast_until > 0.f && last > fmaxf(o.fast_until, tol)) ? kSweepFast
-                        : last > fmaxf(o.round_until, tol)                      ? kSweepRoundQ
-                                                                                : kSweepExact;
-      ChebPlan plan;
-      const bool cheb = o.cheb && nrr > 0 && cheb_plan(lam_h, kc, pb, last, tol, o.cheb_above, &plan);
-      int ncheb = 0, nstep = 0, rc;
-      SweepStep step{};
-      step.Q = w.rr.Z;
-      step.ldq = 2 * pb;
-      step.T = w.T;
-      step.cs = w.rr.cs;
-      step.lam = w.rr.lam;
-      step.next_mode = smode;
-      if (cheb) {
-        // degree j: apply A to X_j, then X_{j+1} from X_j, A X_j and X_{j-1}
-        const int m = std::min(plan.m, budget - 1);
-        double s_prev = plan.s1;
-        for (int j = 0; j < m; ++j, ++it, ++nstep) {
-          double alpha, gamma;
-          if (j == 0) {
-            alpha = plan.s1 / plan.e;
-            gamma = 0.0;
-          } else {
-            const double s_next = 1.0 / (2.0 / plan.s1 - s_prev);
-            alpha = 2.0 * s_next / plan.e;
-            gamma = s_prev * s_next;
-            s_prev = s_next;
-          }
-          step.kind = 2;
-          step.thr = plan.thr;
-          step.a = (float)alpha;
-          step.cc = (float)plan.cc;
-          step.gamma = (float)gamma;
-          if ((rc = apply_op(op, w, d, pb, st, smode, &step, fuse && nstep > 0))) return rc;
+  }
+
+  // Enqueue the cycle's sweeps and the Gram; *ended: the sweep budget is spent (the
+  // iteration is over, nothing was enqueued).
+  int cycle_sweeps(bool* ended) {
+    *ended = !(it - start < max_sweeps);
+    if (*ended) return DEIG_OK;
+    const int budget = max_sweeps - (it - start);
+    // Sweep precision by residual: early sweeps (above fast_until) take S as its
+    // two leading bf16 pieces too - three products, no split in the sweep, ~2^-16
+    // relative (sweep.hip sweep_products SP = 2), 100x below the residual there;
+    // then Q rounded to two pieces (five products) down to round_until; the
+    // closing sweeps exact (the rounding puts ~4e-6 relative noise into the basis
+    // each sweep: a floor under the residual).
+    const int smode = (o.fast_until > 0.f && last > fmaxf(o.fast_until, tol)) ? kSweepFast
+                      : last > fmaxf(o.round_until, tol)                      ? kSweepRoundQ
+                                                                              : kSweepExact;
+    ChebPlan plan;
+    const bool cheb = o.cheb && nrr > 0 && cheb_plan(lam_h, kc, pb, last, tol, o.cheb_above, &plan);
+    int nstep = 0, rc;
+    ncheb_dbg = 0;
+    SweepStep step{};
+    step.Q = w.rr.Z;
+    step.ldq = 2 * pb;
+    step.T = w.T;
+    step.cs = w.rr.cs;
+    step.lam = w.rr.lam;
+    step.next_mode = smode;
+    if (cheb) {
+      // degree j: apply A to X_j, then X_{j+1} from X_j, A X_j and X_{j-1}
+      const int m = std::min(plan.m, budget - 1);
+      double s_prev = plan.s1;
+      for (int j = 0; j < m; ++j, ++it, ++nstep) {
+        double alpha, gamma;
+        if (j == 0) {
+          alpha = plan.s1 / plan.e;
+          gamma = 0.0;
+        } else {
+          const double s_next = 1.0 / (2.0 / plan.s1 - s_prev);
+          alpha = 2.0 * s_next / plan.e;
+          gamma = s_prev * s_next;
+          s_prev = s_next;
         }
-        ncheb = m;
-      } else if (nrr > 0) {
-        const int npow = std::min(rr_every - 1, budget - 1);
-        // power steps on the live Ritz columns of the last RR (Q_j <- Y_j / ||Y w_j||)
-        step.kind = 1;
-        step.tau = tau;
-        for (int j = 0; j < npow; ++j, ++it, ++nstep)
-          if ((rc = apply_op(op, w, d, pb, st, smode, &step, fuse && nstep > 0))) return rc;
+        step.kind = 2;
+        step.thr = plan.thr;
+        step.a = (float)alpha;
+        step.cc = (float)plan.cc;
+        step.gamma = (float)gamma;
+        if ((rc = apply_op(op, w, d, pb, st, smode, &step, fuse && nstep > 0))) return rc;
       }
-      if ((rc = apply_op(op, w, d, pb, st, smode, nullptr, fuse && nstep > 0))) return rc;
-      ++it;
-      if ((rc = skinny_launch(true, w.rr.Z, 2 * pb, w.rr.Z, 2 * pb, w.rr.C, 2 * pb, 2 * pb, 2 * pb,
-                              d, 1.f, 0.f, w.slab, w.slab_bytes, st)))
-        return rc;
-      // The next basis Y W spans span(Y) for any invertible W, so subspace progress
-      // does not need converged Ritz vectors; the residual of approximate pairs
-      // only over-states the error (no false convergence).
-      const int jcap = (jcap_sweeps > 0 && last > jcap_above) ? jcap_sweeps : 30;
-      if ((rc = rr_small_launch(w.rr, pb, st, jcap))) return rc;
-      if ((rc = rr_update_launch(w.rr, d, pb, kc, Vb, ldv, evb, st))) return rc;
-      int jconv_h = 1;  // the RR's Jacobi converged (rr.hip info[3])
-      DEIG_HIP_CHECK(
-          hipMemcpyAsync(res_h, w.rr.resid, sizeof(float) * (kc + 1), hipMemcpyDeviceToHost, st));
-      DEIG_HIP_CHECK(hipMemcpyAsync(lam_h, w.rr.lam, sizeof(float) * pb, hipMemcpyDeviceToHost, st));
-      if (jcap < 30)
-        DEIG_HIP_CHECK(
-            hipMemcpyAsync(&jconv_h, w.rr.info + 3, sizeof(int), hipMemcpyDeviceToHost, st));
-      DEIG_HIP_CHECK(hipStreamSynchronize(st));
-      last = res_h[kc];
-      // Ritz pairs of a capped Jacobi that stopped short are approximate: their
-      // residual bounds the error, but the eigenvalues / vectors returned are those
-      // of an unconverged small solve, so no exit is taken on them - the next RR
-      // (the residual is then below jcap_above) runs the Jacobi to convergence.
-      // Needed where the residual is relative to a dominant theta_0 (worker S:
-      // r02s, a 2-sweep cap at every residual missed a CIFAR-gray eigenvalue by
-      // 1.0046e-5); the server's projector average (eigenvalues in [0, 1], top k
-      // near 1) exits as before - guarding it cost c1's server 5 -> 7 sweeps.
-      const bool exact_rr = jconv_h != 0 || op.implicit;
-      ++nrr;
-      if (o.debug) {
-        int inf[9] = {0};
-        DEIG_HIP_CHECK(hipMemcpy(inf, w.rr.info, sizeof(inf), hipMemcpyDeviceToHost));
-        fprintf(stderr, "[deig] d=%lld k=%d p=%d sweep %d resid %.3e cheb_deg %d chol_floor %d "
-                "jacobi_sweeps %d rotations %d small-solve us: chol %.1f linv %.1f congr %.1f "
-                "jacobi %.1f tail %.1f\n",
-                (long long)d, kc, pb, it, last, ncheb, inf[0], inf[1], inf[2], inf[4] * 0.01,
-                (inf[5] - inf[4]) * 0.01, (inf[6] - inf[5]) * 0.01, (inf[7] - inf[6]) * 0.01,
-                (inf[8] - inf[7]) * 0.01);
-      }
-      if (!(last == last) || last > 3.0e38f)  // NaN / Inf
-        return fail(DEIG_EINVAL, "solver: non-finite residual (input contains NaN/Inf?)");
-      if (!exact_rr) continue;
-      if (last <= tol) {
-        converged = true;
+      ncheb_dbg = m;
+    } else if (nrr > 0) {
+      const int npow = std::min(rr_every - 1, budget - 1);
+      // power steps on the live Ritz columns of the last RR (Q_j <- Y_j / ||Y w_j||)
+      step.kind = 1;
+      step.tau = tau;
+      for (int j = 0; j < npow; ++j, ++it, ++nstep)
+        if ((rc = apply_op(op, w, d, pb, st, smode, &step, fuse && nstep > 0))) return rc;
+    }
+    if ((rc = apply_op(op, w, d, pb, st, smode, nullptr, fuse && nstep > 0))) return rc;
+    ++it;
+    // The next basis Y W spans span(Y) for any invertible W, so subspace progress
+    // does not need converged Ritz vectors; the residual of approximate pairs only
+    // over-states the error (no false convergence).
+    jcap = (jcap_sweeps > 0 && last > jcap_above) ? jcap_sweeps : 30;
+    return skinny_launch(true, w.rr.Z, 2 * pb, w.rr.Z, 2 * pb, w.rr.C, 2 * pb, 2 * pb, 2 * pb, d, 1.f,
+                         0.f, w.slab, w.slab_bytes, st);
+  }
+
+  int cycle_rr_small() { return rr_small_launch(w.rr, pb, st, jcap); }
+
+  // Ritz vectors / residuals and their copies to the host (read after a sync).
+  int cycle_update() {
+    int rc;
+    if ((rc = rr_update_launch(w.rr, d, pb, kc, Vb, ldv, evb, st))) return rc;
+    jconv_h = 1;
+    DEIG_HIP_CHECK(
+        hipMemcpyAsync(res_h, w.rr.resid, sizeof(float) * (kc + 1), hipMemcpyDeviceToHost, st));
+    DEIG_HIP_CHECK(hipMemcpyAsync(lam_h, w.rr.lam, sizeof(float) * pb, hipMemcpyDeviceToHost, st));
+    if (jcap < 30)
+      DEIG_HIP_CHECK(hipMemcpyAsync(&jconv_h, w.rr.info + 3, sizeof(int), hipMemcpyDeviceToHost, st));
+    return DEIG_OK;
+  }
+
+  // After the sync: *done = the iteration is over (converged, early exit or stalled).
+  int cycle_finish(bool* done) {
+    *done = false;
+    last = res_h[kc];
+    // Ritz pairs of a capped Jacobi that stopped short are approximate: their
+    // residual bounds the error, but the eigenvalues / vectors returned are those
+    // of an unconverged small solve, so no exit is taken on them - the next RR
+    // (the residual is then below jcap_above) runs the Jacobi to convergence.
+    // Needed where the residual is relative to a dominant theta_0 (worker S:
+    // r02s, a 2-sweep cap at every residual missed a CIFAR-gray eigenvalue by
+    // 1.0046e-5); the server's projector average (eigenvalues in [0, 1], top k
+    // near 1) exits as before - guarding it cost c1's server 5 -> 7 sweeps.
+    const bool exact_rr = jconv_h != 0 || op.implicit;
+    ++nrr;
+    if (o.debug) {
+      int inf[9] = {0};
+      DEIG_HIP_CHECK(hipMemcpy(inf, w.rr.info, sizeof(inf), hipMemcpyDeviceToHost));
+      fprintf(stderr, "[deig] d=%lld k=%d p=%d sweep %d resid %.3e cheb_deg %d chol_floor %d "
+              "jacobi_sweeps %d rotations %d small-solve us: chol %.1f linv %.1f congr %.1f "
+              "jacobi %.1f tail %.1f\n",
+              (long long)d, kc, pb, it, last, ncheb_dbg, inf[0], inf[1], inf[2], inf[4] * 0.01,
+              (inf[5] - inf[4]) * 0.01, (inf[6] - inf[5]) * 0.01, (inf[7] - inf[6]) * 0.01,
+              (inf[8] - inf[7]) * 0.01);
+    }
+    if (!(last == last) || last > 3.0e38f)  // NaN / Inf
+      return fail(DEIG_EINVAL, "solver: non-finite residual (input contains NaN/Inf?)");
+    if (!exact_rr) return DEIG_OK;
+    if (last <= tol) {
+      converged = true;
+      *done = true;
+      return DEIG_OK;
+    }
+    if (allow_early) {
+      const int r = dominant(kc);
+      bool ok = r >= 1;
+      for (int j = 0; j < r && ok; ++j) ok = res_h[j] <= tol;
+      if (ok) {
+        early = true;
+        *done = true;
         return DEIG_OK;
       }
-      if (allow_early) {
-        const int r = dominant(kc);
-        bool ok = r >= 1;
-        for (int j = 0; j < r && ok; ++j) ok = res_h[j] <= tol;
-        if (ok) {
-          *early_out = true;
-          return DEIG_OK;
-        }
+    }
+    // Stagnation: no 10% improvement over the best residual for 4 Rayleigh-Ritz
+    // steps in a row.  It counts as convergence only at the fp32 floor (residual
+    // within kStallAccept* of tol); a stall above it is slow convergence (a small
+    // eigengap at k), so the iteration goes on and, if it stays stuck for
+    // kStallGiveUp RR steps, stops early with DEIG_NOT_CONVERGED.
+    if (last < 0.9f * best) {
+      best = last;
+      since_best = 0;
+    } else if (++since_best >= 4 && it - start >= 8) {
+      if (last <= fmaxf(kStallAcceptTol * tol, kStallAcceptAbs)) {
+        converged = true;
+        *done = true;
+        return DEIG_OK;
       }
-      // Stagnation: no 10% improvement over the best residual for 4 Rayleigh-Ritz
-      // steps in a row.  It counts as convergence only at the fp32 floor (residual
-      // within kStallAccept* of tol); a stall above it is slow convergence (a small
-      // eigengap at k), so the iteration goes on and, if it stays stuck for
-      // kStallGiveUp RR steps, stops early with DEIG_NOT_CONVERGED.
-      if (last < 0.9f * best) {
-        best = last;
-        since_best = 0;
-      } else if (++since_best >= 4 && it - start >= 8) {
-        if (last <= fmaxf(kStallAcceptTol * tol, kStallAcceptAbs)) {
-          converged = true;
-          return DEIG_OK;
-        }
-        if (since_best >= kStallGiveUp) return DEIG_OK;
-      }
+      if (since_best >= kStallGiveUp) *done = true;
     }
     return DEIG_OK;
   }
 
   // (Re)build the sweep image of the current operator (explicit S only).
-  int prepare(int pb) {
+  int prepare(int pb_) {
     if (!w.sweep_ws) return DEIG_OK;
-    return sweep_prepare(op.S, op.stype, d, op.lds, pb, w.sweep_ws, w.sweep_bytes, st, op.Vd,
+    return sweep_prepare(op.S, op.stype, d, op.lds, pb_, w.sweep_ws, w.sweep_bytes, st, op.Vd,
                          op.ldvd, op.lamd, op.r, op.shift);
   }
 };
@@ -526,119 +571,366 @@ void block_shape(int64_t d, int k, int p_in, int* p_blk, int* kb) {
 // to cancellation.  Deflated images are formed in double (sweep_prepare_kernel).
 // A block whose Ritz values show a large negative eigenvalue (S indefinite: the
 // filter and power steps favour large |lambda|) restarts the solve on S + sigma I.
-int solve(const Operator& op0, int64_t d, int k, int p, int max_sweeps, float tol, const float* Q0,
-          int k0, int64_t ldq0, float* V, int64_t ldv, float* evals, int* sweeps_out,
-          float* resid_out, const Opts& o, void* ws, size_t ws_bytes, hipStream_t st) {
-  DEIG_REQUIRE(d >= 16 && d % 4 == 0, "solver: d=%lld must be >= 16 and a multiple of 4",
-               (long long)d);
-  DEIG_REQUIRE(k >= 1 && k <= d, "solver: need 1 <= k <= d (k=%d, d=%lld)", k, (long long)d);
-  int pb0, kb;
-  block_shape(d, k, p, &pb0, &kb);
-  if (k <= kMaxP)
-    DEIG_REQUIRE(pb0 % 16 == 0 && pb0 >= k && pb0 <= kMaxP && pb0 <= d,
-                 "solver: subspace p=%d must be a multiple of 16 with k <= p <= min(128, d)", pb0);
-  else
-    DEIG_REQUIRE(pb0 % 16 == 0 && pb0 >= 2 * kGuard && pb0 <= kMaxP && pb0 <= d,
-                 "solver: k=%d > 128 needs a block subspace p in {32, ..., 128} (p=%d)", k, pb0);
-  DEIG_REQUIRE(max_sweeps >= 1, "solver: max_sweeps must be >= 1");
-  DEIG_REQUIRE(V && evals && ldv >= d, "solver: bad V / evals / ldv");
-  DEIG_REQUIRE(k0 >= 0 && k0 <= pb0 && (k0 == 0 || (Q0 && ldq0 >= d)), "solver: bad warm start");
-  const bool image = !op0.implicit && o.sweep_algo != DEIG_SWEEP_FP32;
-  DEIG_REQUIRE(image || op0.implicit || op0.stype == DEIG_F32,
-               "solver: a float64 S needs the bf16x6 sweep (DEIG_SWEEP_AUTO)");
-  size_t total = 0;
+//   Written as a state machine so that several independent problems can advance in
+// lockstep (solve_batch): BLOCK (set up the next block: image, start basis) ->
+// CYCLE (Solver cycles until the iteration ends) -> end_block (lock / redo /
+// restart / next block) ... -> FINAL (eigenvalues) -> DONE.
+struct SolveSM {
+  enum State { BLOCK, CYCLE, FINAL, DONE };
+  Operator op0;
+  int64_t d = 0;
+  int k = 0, pb0 = 0, kb = 0, k0 = 0;
+  const float* Q0 = nullptr;
+  int64_t ldq0 = 0;
+  float* V = nullptr;
+  int64_t ldv = 0;
+  float* evals = nullptr;
   Solver sv;
-  sv.w = carve_solver(ws, ws_bytes, d, kb, k, pb0, op0.implicit ? op0.mk : 0, image, &total);
-  if (!ws || total > ws_bytes)
-    return fail(DEIG_EWORKSPACE, "solver: workspace %zu bytes < required %zu", ws_bytes, total);
-  sv.op = op0;
-  sv.o = o;
-  sv.d = d;
-  sv.max_sweeps = max_sweeps;
-  sv.tol = tol;
-  sv.st = st;
-  const bool can_deflate = o.deflate && !op0.implicit && k >= 2;
+  bool can_deflate = false;
   double shift = 0.0;
   float scale = 0.f;  // |theta| scale of the operator (first block's Ritz values)
   bool all_conv = true;
   float worst = 0.f;
+  int attempt = 0;
+  int locked = 0;     // pairs locked at V columns [k - locked, k)
+  bool redo = false;  // re-iterate the rest of a block after locking its dominant pairs
+  int warm = 0;       // redo: columns of the block computed before (just below locked)
+  int kc = 0, pb = 0;
+  float* Vb = nullptr;
+  float* evb = nullptr;
+  State state = BLOCK;
   int rc = DEIG_OK;
-  for (int attempt = 0;; ++attempt) {
-    all_conv = true;
-    worst = 0.f;
-    bool restart = false;
-    int locked = 0;     // pairs locked at V columns [k - locked, k)
-    bool redo = false;  // re-iterate the rest of a block after locking its dominant pairs
-    int warm = 0;       // redo: columns of the block computed before (just below locked)
-    while (locked < k) {
-      const int rem = k - locked;
-      const int kc = rem <= kb ? rem : kb;
-      // the last block of k > 128 pairs: the default subspace for its size
-      const int pb = (rem <= kb && k > kMaxP) ? std::min(default_subspace(d, kc), pb0) : pb0;
-      float* Vb = V + (int64_t)(k - locked - kc) * ldv;
-      float* evb = evals + (k - locked - kc);
-      sv.op.shift = shift;
-      sv.op.r = locked;
-      sv.op.Vd = locked ? V + (int64_t)(k - locked) * ldv : nullptr;
-      sv.op.ldvd = ldv;
-      sv.op.lamd = locked ? evals + (k - locked) : nullptr;
-      if ((rc = sv.prepare(pb))) break;
-      if (redo) {  // warm start: the block's columns below the dominant pairs
-        rc = rr_init_launch(sv.w.rr.Z, d, pb, V + (int64_t)(k - locked - warm) * ldv, warm, ldv,
-                            0x5eed5eefull + locked, st);
-      } else if (locked == 0 && k <= kMaxP) {
-        rc = rr_init_launch(sv.w.rr.Z, d, pb, Q0, k0, ldq0, 0x5eed5eedull, st);
-      } else {
-        rc = rr_init_launch(sv.w.rr.Z, d, pb, nullptr, 0, 0, 0x5eed5eedull + locked, st);
+
+  int init(const Operator& op, int64_t d_, int k_, int p, int max_sweeps, float tol, const float* Q0_,
+           int k0_, int64_t ldq0_, float* V_, int64_t ldv_, float* evals_, const Opts& o, void* ws,
+           size_t ws_bytes, hipStream_t st) {
+    d = d_;
+    k = k_;
+    DEIG_REQUIRE(d >= 16 && d % 4 == 0, "solver: d=%lld must be >= 16 and a multiple of 4",
+                 (long long)d);
+    DEIG_REQUIRE(k >= 1 && k <= d, "solver: need 1 <= k <= d (k=%d, d=%lld)", k, (long long)d);
+    block_shape(d, k, p, &pb0, &kb);
+    if (k <= kMaxP)
+      DEIG_REQUIRE(pb0 % 16 == 0 && pb0 >= k && pb0 <= kMaxP && pb0 <= d,
+                   "solver: subspace p=%d must be a multiple of 16 with k <= p <= min(128, d)", pb0);
+    else
+      DEIG_REQUIRE(pb0 % 16 == 0 && pb0 >= 2 * kGuard && pb0 <= kMaxP && pb0 <= d,
+                   "solver: k=%d > 128 needs a block subspace p in {32, ..., 128} (p=%d)", k, pb0);
+    DEIG_REQUIRE(max_sweeps >= 1, "solver: max_sweeps must be >= 1");
+    DEIG_REQUIRE(V_ && evals_ && ldv_ >= d, "solver: bad V / evals / ldv");
+    DEIG_REQUIRE(k0_ >= 0 && k0_ <= pb0 && (k0_ == 0 || (Q0_ && ldq0_ >= d)), "solver: bad warm start");
+    const bool image = !op.implicit && o.sweep_algo != DEIG_SWEEP_FP32;
+    DEIG_REQUIRE(image || op.implicit || op.stype == DEIG_F32,
+                 "solver: a float64 S needs the bf16x6 sweep (DEIG_SWEEP_AUTO)");
+    size_t total = 0;
+    sv.w = carve_solver(ws, ws_bytes, d, kb, k, pb0, op.implicit ? op.mk : 0, image, &total);
+    if (!ws || total > ws_bytes)
+      return fail(DEIG_EWORKSPACE, "solver: workspace %zu bytes < required %zu", ws_bytes, total);
+    op0 = op;
+    sv.op = op;
+    sv.o = o;
+    sv.d = d;
+    sv.max_sweeps = max_sweeps;
+    sv.tol = tol;
+    sv.st = st;
+    Q0 = Q0_;
+    k0 = k0_;
+    ldq0 = ldq0_;
+    V = V_;
+    ldv = ldv_;
+    evals = evals_;
+    can_deflate = o.deflate && !op.implicit && k >= 2;
+    state = BLOCK;
+    return DEIG_OK;
+  }
+
+  // BLOCK: the next block's operator, sweep image and start basis; -> CYCLE or FINAL.
+  int start_block() {
+    if (locked >= k) {
+      state = FINAL;
+      return DEIG_OK;
+    }
+    const int rem = k - locked;
+    kc = rem <= kb ? rem : kb;
+    // the last block of k > 128 pairs: the default subspace for its size
+    pb = (rem <= kb && k > kMaxP) ? std::min(default_subspace(d, kc), pb0) : pb0;
+    Vb = V + (int64_t)(k - locked - kc) * ldv;
+    evb = evals + (k - locked - kc);
+    sv.op.shift = shift;
+    sv.op.r = locked;
+    sv.op.Vd = locked ? V + (int64_t)(k - locked) * ldv : nullptr;
+    sv.op.ldvd = ldv;
+    sv.op.lamd = locked ? evals + (k - locked) : nullptr;
+    int r;
+    if ((r = sv.prepare(pb))) return r;
+    if (redo) {  // warm start: the block's columns below the dominant pairs
+      r = rr_init_launch(sv.w.rr.Z, d, pb, V + (int64_t)(k - locked - warm) * ldv, warm, ldv,
+                         0x5eed5eefull + locked, sv.st);
+    } else if (locked == 0 && k <= kMaxP) {
+      r = rr_init_launch(sv.w.rr.Z, d, pb, Q0, k0, ldq0, 0x5eed5eedull, sv.st);
+    } else {
+      r = rr_init_launch(sv.w.rr.Z, d, pb, nullptr, 0, 0, 0x5eed5eedull + locked, sv.st);
+    }
+    if (r) return r;
+    sv.iter_begin(kc, pb, Vb, ldv, evb, can_deflate && sv.o.deflate_early && !redo);
+    state = CYCLE;
+    return DEIG_OK;
+  }
+
+  // The block's iteration has ended: lock / redo / restart / next block.
+  int end_block() {
+    int r;
+    if (locked > 0 && (r = deflate_orth_launch(Vb, ldv, d, kc, locked, sv.st))) return r;
+    if (locked == 0 && attempt == 0) scale = fmaxf(fabsf(sv.lam_h[0]), fabsf(sv.lam_h[pb - 1]));
+    // Indefinite S: the most negative Ritz value of the block against the block's
+    // target (and the operator's scale - deflation residue is ~1e-7 of it).
+    const float tmin = sv.lam_h[pb - 1];
+    if (!op0.implicit && attempt < kMaxShifts &&
+        tmin < -fmaxf(kNegRel * scale, kNegTarget * fmaxf(sv.lam_h[kc - 1], 0.f))) {
+      shift = kShiftGrow * (shift - (double)tmin);  // |theta_min| of the shifted op
+      if (sv.o.debug)
+        fprintf(stderr, "[deig] negative Ritz value %.4e: restarting on S + %.4e I\n", tmin, shift);
+      ++attempt;
+      all_conv = true;
+      worst = 0.f;
+      locked = 0;
+      redo = false;
+      warm = 0;
+      state = BLOCK;
+      return DEIG_OK;
+    }
+    const int nd = (can_deflate && !redo && (sv.converged || sv.early)) ? sv.dominant(kc) : 0;
+    if (sv.o.debug && nd)
+      fprintf(stderr, "[deig] locking %d dominant pair(s)%s at sweep %d\n", nd,
+              sv.early ? " (early)" : "", sv.it);
+    if (nd >= 1 && nd < kc) {
+      locked += nd;  // the rest of the block is iterated again (warm) below them
+      warm = kc - nd;
+      redo = true;
+      state = BLOCK;
+      return DEIG_OK;
+    }
+    worst = fmaxf(worst, sv.last);
+    if (!sv.converged) all_conv = false;
+    locked += kc;
+    redo = false;
+    state = BLOCK;
+    return DEIG_OK;
+  }
+
+  // FINAL: eigenvalues - double-precision Rayleigh quotients on S itself (explicit
+  // S; they need no unshift), the projector average's fp32 Ritz values unshifted.
+  int finalize() {
+    int r = DEIG_OK;
+    if (!op0.implicit)
+      r = rq_launch(op0.S, op0.stype, d, op0.lds, V, ldv, k, evals, sv.w.rq, sv.st);
+    else if (shift != 0.0)
+      r = unshift_launch(evals, k, shift, sv.st);
+    state = DONE;
+    return r;
+  }
+
+  // Advance through the non-cycling states until CYCLE or DONE.
+  int settle() {
+    int r;
+    while (state == BLOCK || state == FINAL) {
+      if (state == BLOCK) {
+        if ((r = start_block())) return r;
+      } else if ((r = finalize())) {
+        return r;
       }
-      if (rc) break;
-      bool early = false;
-      const bool allow_early = can_deflate && o.deflate_early && !redo;
-      if ((rc = sv.iterate(kc, pb, Vb, ldv, evb, allow_early, &early))) break;
-      if (locked > 0 && (rc = deflate_orth_launch(Vb, ldv, d, kc, locked, st))) break;
-      if (locked == 0 && attempt == 0)
-        scale = fmaxf(fabsf(sv.lam_h[0]), fabsf(sv.lam_h[pb - 1]));
-      // Indefinite S: the most negative Ritz value of the block against the block's
-      // target (and the operator's scale - deflation residue is ~1e-7 of it).
-      const float tmin = sv.lam_h[pb - 1];
-      if (!op0.implicit && attempt < kMaxShifts &&
-          tmin < -fmaxf(kNegRel * scale, kNegTarget * fmaxf(sv.lam_h[kc - 1], 0.f))) {
-        shift = kShiftGrow * ((double)shift - (double)tmin);  // |theta_min| of the shifted op
-        if (o.debug)
-          fprintf(stderr, "[deig] negative Ritz value %.4e: restarting on S + %.4e I\n", tmin, shift);
-        restart = true;
-        break;
-      }
-      const int r = (can_deflate && !redo && (sv.converged || early)) ? sv.dominant(kc) : 0;
-      if (o.debug && r)
-        fprintf(stderr, "[deig] locking %d dominant pair(s)%s at sweep %d\n", r,
-                early ? " (early)" : "", sv.it);
-      if (r >= 1 && r < kc) {
-        locked += r;  // the rest of the block is iterated again (warm) below them
-        warm = kc - r;
-        redo = true;
+    }
+    return DEIG_OK;
+  }
+
+  int outcome(int* sweeps_out, float* resid_out) const {
+    if (sweeps_out) *sweeps_out = sv.it;
+    if (resid_out) *resid_out = rc ? sv.last : worst;
+    if (rc) return rc;
+    if (!all_conv)
+      return fail(DEIG_NOT_CONVERGED, "solver: residual %g > tol %g after %d sweeps%s", worst,
+                  sv.tol, sv.it, " (eigengap at k too small for the sweep budget, or stalled)");
+    return DEIG_OK;
+  }
+};
+
+int solve(const Operator& op0, int64_t d, int k, int p, int max_sweeps, float tol, const float* Q0,
+          int k0, int64_t ldq0, float* V, int64_t ldv, float* evals, int* sweeps_out,
+          float* resid_out, const Opts& o, void* ws, size_t ws_bytes, hipStream_t st) {
+  SolveSM sm;
+  int rc = sm.init(op0, d, k, p, max_sweeps, tol, Q0, k0, ldq0, V, ldv, evals, o, ws, ws_bytes, st);
+  if (rc) return rc;
+  while (!rc && sm.state != SolveSM::DONE) {
+    if ((rc = sm.settle()) || sm.state == SolveSM::DONE) break;
+    bool ended = false, done = false;
+    if ((rc = sm.sv.cycle_sweeps(&ended))) break;
+    if (ended) {
+      rc = sm.end_block();
+      continue;
+    }
+    if ((rc = sm.sv.cycle_rr_small()) || (rc = sm.sv.cycle_update())) break;
+    if (hipStreamSynchronize(st) != hipSuccess) {
+      rc = fail(DEIG_EHIP, "solver: stream synchronisation failed");
+      break;
+    }
+    if ((rc = sm.sv.cycle_finish(&done))) break;
+    if (done) rc = sm.end_block();
+  }
+  sm.rc = rc;
+  return sm.outcome(sweeps_out, resid_out);
+}
+
+// W independent explicit-S problems (same d, k, p) advanced in lockstep.  One host
+// thread per problem enqueues that problem's sweeps, Gram and updates on its own
+// stream (one thread issuing every problem's launches was host-bound: ~15 launches
+// per problem and round, r03l); at each Rayleigh-Ritz step the threads meet at a
+// barrier and the last one to arrive launches the small solves of all arrived
+// problems in ONE launch (one workgroup each, on `st`, after every participant's
+// Gram), which each then waits for on its own stream.  A problem that is between
+// blocks joins the next round; one that is done leaves the barrier.  Results are
+// those of W separate solve() calls (same kernels, same decisions, tested bit for
+// bit); what changes is that W single-workgroup solves share a launch instead of W
+// streams contending for the hardware queues.
+int solve_batch(int W, const Operator* ops, int64_t d, int k, int p, int max_sweeps, float tol,
+                float* const* V, int64_t ldv, float* const* evals, int* sweeps_out, float* resid_out,
+                const Opts& o, char* ws, size_t ws_each, const hipStream_t* streams, hipStream_t st) {
+  DEIG_REQUIRE(W >= 1 && W <= 1024, "solve_batch: W=%d out of range", W);
+  int dev = 0;
+  DEIG_HIP_CHECK(hipGetDevice(&dev));
+  std::vector<SolveSM> sm(W);
+  std::vector<hipEvent_t> ev(W + 1, nullptr);
+  int rc = DEIG_OK;
+  for (int i = 0; i <= W && !rc; ++i)
+    if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess)
+      rc = fail(DEIG_EHIP, "solve_batch: event creation failed");
+  for (int i = 0; i < W && !rc; ++i)
+    rc = sm[i].init(ops[i], d, k, p, max_sweeps, tol, nullptr, 0, 0, V[i], ldv, evals[i], o,
+                    ws + (size_t)i * ws_each, ws_each, streams[i]);
+  if (rc) {
+    for (hipEvent_t e : ev)
+      if (e) (void)hipEventDestroy(e);
+    return rc;
+  }
+  struct Coord {
+    std::mutex mu;
+    std::condition_variable cv;
+    int active = 0;          // problems not finished
+    std::vector<int> here;   // problems waiting at the barrier of this generation
+    long gen = 0;
+    int err = DEIG_OK;
+    char msg[1024] = "";
+  } co;
+  co.active = W;
+  std::vector<int> jc;
+  std::vector<const RRBuffers*> bufs;
+  // with co.mu held: the small solves of every waiting problem, then release them
+  auto launch_round = [&]() {
+    int r = DEIG_OK;
+    for (int i : co.here)
+      if (hipStreamWaitEvent(st, ev[i], 0) != hipSuccess)
+        r = fail(DEIG_EHIP, "solve_batch: stream wait failed");
+    // one launch per subspace width (the last block of k > 128 pairs may be narrower)
+    for (size_t a = 0; a < co.here.size() && !r; ++a) {
+      const int pw = sm[co.here[a]].sv.pb;
+      bool seen = false;
+      for (size_t b = 0; b < a; ++b) seen |= sm[co.here[b]].sv.pb == pw;
+      if (seen) continue;
+      bufs.clear();
+      jc.clear();
+      for (int i : co.here)
+        if (sm[i].sv.pb == pw) {
+          bufs.push_back(&sm[i].sv.w.rr);
+          jc.push_back(sm[i].sv.jcap);
+        }
+      r = rr_small_batch_launch(bufs.data(), jc.data(), (int)bufs.size(), pw, st);
+    }
+    if (!r && hipEventRecord(ev[W], st) != hipSuccess) r = fail(DEIG_EHIP, "solve_batch: event record failed");
+    if (r && !co.err) {
+      co.err = r;
+      snprintf(co.msg, sizeof(co.msg), "%s", g_err);
+    }
+    co.here.clear();
+    ++co.gen;
+    co.cv.notify_all();
+  };
+  auto run = [&](int i) {
+    (void)hipSetDevice(dev);  // HIP's current device is per thread
+    SolveSM& m = sm[i];
+    int r = DEIG_OK;
+    while (!r) {
+      if ((r = m.settle()) || m.state == SolveSM::DONE) break;
+      bool ended = false, done = false;
+      if ((r = m.sv.cycle_sweeps(&ended))) break;
+      if (ended) {
+        r = m.end_block();
         continue;
       }
-      worst = fmaxf(worst, sv.last);
-      if (!sv.converged) all_conv = false;
-      locked += kc;
-      redo = false;
+      if (hipEventRecord(ev[i], streams[i]) != hipSuccess) {
+        r = fail(DEIG_EHIP, "solve_batch: event record failed");
+        break;
+      }
+      {
+        std::unique_lock<std::mutex> lk(co.mu);
+        if (co.err) break;
+        co.here.push_back(i);
+        const long g = co.gen;
+        if ((int)co.here.size() == co.active)
+          launch_round();
+        else
+          co.cv.wait(lk, [&] { return co.gen != g || co.err != DEIG_OK; });
+        if (co.err) break;
+      }
+      if (hipStreamWaitEvent(streams[i], ev[W], 0) != hipSuccess) {
+        r = fail(DEIG_EHIP, "solve_batch: stream wait failed");
+        break;
+      }
+      if ((r = m.sv.cycle_update())) break;
+      if (hipStreamSynchronize(streams[i]) != hipSuccess) {
+        r = fail(DEIG_EHIP, "solve_batch: stream synchronisation failed");
+        break;
+      }
+      if ((r = m.sv.cycle_finish(&done))) break;
+      if (done) r = m.end_block();
     }
-    if (rc || !restart) break;
+    std::lock_guard<std::mutex> lk(co.mu);
+    m.rc = r;
+    --co.active;
+    if (r && !co.err) {
+      co.err = r;
+      snprintf(co.msg, sizeof(co.msg), "%s", g_err);
+    }
+    if (!co.err && !co.here.empty() && (int)co.here.size() == co.active) launch_round();
+    co.cv.notify_all();
+  };
+  std::vector<std::thread> th;
+  th.reserve(W - 1);
+  for (int i = 1; i < W; ++i) th.emplace_back(run, i);
+  run(0);
+  for (std::thread& t : th) t.join();
+  // every problem's last kernels (eigenvalues) are on its stream: join them into st
+  for (int i = 0; i < W; ++i)
+    if (hipEventRecord(ev[i], streams[i]) == hipSuccess) (void)hipStreamWaitEvent(st, ev[i], 0);
+  for (hipEvent_t e : ev)
+    if (e) (void)hipEventDestroy(e);
+  if (co.err) {
+    set_error("%s", co.msg);
+    for (int i = 0; i < W; ++i) {
+      if (sweeps_out) sweeps_out[i] = sm[i].sv.it;
+      if (resid_out) resid_out[i] = sm[i].sv.last;
+    }
+    return co.err;
   }
-  // eigenvalues: double-precision Rayleigh quotients on S itself (explicit S; they
-  // need no unshift), the projector average's fp32 Ritz values unshifted
-  if (!rc && !op0.implicit)
-    rc = rq_launch(op0.S, op0.stype, d, op0.lds, V, ldv, k, evals, sv.w.rq, st);
-  else if (!rc && shift != 0.0)
-    rc = unshift_launch(evals, k, shift, st);
-  if (sweeps_out) *sweeps_out = sv.it;
-  if (resid_out) *resid_out = rc ? sv.last : worst;
-  if (rc) return rc;
-  if (!all_conv)
-    return fail(DEIG_NOT_CONVERGED, "solver: residual %g > tol %g after %d sweeps%s", worst, tol,
-                sv.it, " (eigengap at k too small for the sweep budget, or stalled)");
-  return DEIG_OK;
+  int first = DEIG_OK;
+  char msg[1024] = "";
+  for (int i = 0; i < W; ++i) {
+    const int r = sm[i].outcome(sweeps_out ? sweeps_out + i : nullptr, resid_out ? resid_out + i : nullptr);
+    if (r && !first) {
+      first = r;
+      snprintf(msg, sizeof(msg), "%s", g_err);
+    }
+  }
+  if (first) set_error("%s", msg);
+  return first;
 }
 
 }  // namespace
@@ -781,6 +1073,43 @@ int deig_topk_sym_f32(const float* S, int64_t d, int64_t lds, int k, int p, int 
                       void* stream) {
   return deig_topk_sym_ex(S, DEIG_F32, d, lds, k, p, max_sweeps, tol, Q0, k0, ldq0, V, ldv, evals,
                           sweeps_out, resid_out, nullptr, ws, ws_bytes, stream);
+}
+
+size_t deig_topk_batch_workspace(int W, int64_t d, int k, int p, int stype,
+                                 const deig_solver_opts* opts) {
+  (void)stype;
+  if (W < 1) return 0;
+  return (size_t)W * align_up(topk_ws(d, k, p, false, 0, opts), 256);
+}
+
+int deig_topk_sym_batch(int W, const void* const* S, int stype, int64_t d, int64_t lds, int k, int p,
+                        int max_sweeps, float tol, float* const* V, int64_t ldv, float* const* evals,
+                        int* sweeps_out, float* resid_out, const deig_solver_opts* opts, void* ws,
+                        size_t ws_bytes, void* const* streams, void* stream) {
+  g_err[0] = 0;
+  if (int rc = check_opts(opts)) return rc;
+  if (W < 1 || !S || !V || !evals) return fail(DEIG_EINVAL, "topk_batch: need W >= 1 and S / V / evals arrays");
+  if (stype != DEIG_F32 && stype != DEIG_F64)
+    return fail(DEIG_EINVAL, "topk_batch: unknown element type %d", stype);
+  for (int i = 0; i < W; ++i)
+    if (!S[i] || lds < d || lds % 4 != 0 || !aligned16(S[i]))
+      return fail(DEIG_EINVAL, "topk_batch: S[%d] must be 16-byte aligned with lds >= d, lds %% 4 == 0", i);
+  const size_t each = align_up(topk_ws(d, k, p, false, 0, opts), 256);
+  if (!ws || ws_bytes < (size_t)W * each)
+    return fail(DEIG_EWORKSPACE, "topk_batch: workspace %zu bytes < required %zu", ws_bytes,
+                (size_t)W * each);
+  std::vector<Operator> ops(W);
+  std::vector<hipStream_t> sts(W);
+  for (int i = 0; i < W; ++i) {
+    ops[i] = Operator{};
+    ops[i].implicit = false;
+    ops[i].S = S[i];
+    ops[i].stype = stype;
+    ops[i].lds = lds;
+    sts[i] = streams && streams[i] ? (hipStream_t)streams[i] : (hipStream_t)stream;
+  }
+  return solve_batch(W, ops.data(), d, k, p, max_sweeps, tol, V, ldv, evals, sweeps_out, resid_out,
+                     make_opts(opts), static_cast<char*>(ws), each, sts.data(), (hipStream_t)stream);
 }
 
 size_t deig_projavg_workspace_ex(int64_t d, int64_t mk, int k, int p,

@@ -154,6 +154,10 @@ int rr_init_launch(float* Z, int64_t d, int p, const float* Q0, int k0, int64_t 
 // jrel: a pair is rotated while |h_ab| > jrel sqrt(|h_aa h_bb|) (2e-7: to rounding).
 int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream, int max_jsweeps = 30,
                     float jrel = 2e-7f);
+// n independent small solves in launches of up to kRRBatch workgroups (one each).
+constexpr int kRRBatch = 16;
+int rr_small_batch_launch(const RRBuffers* const* bs, const int* max_jsweeps, int n, int p,
+                          hipStream_t stream, float jrel = 2e-7f);
 int rr_update_blocks(int64_t d);
 int rr_power_launch(const RRBuffers& b, int64_t d, int p, float tau, hipStream_t stream);
 // One scaled Chebyshev filter degree on Z = [X_j | A X_j] with T = X_{j-1} (d x p).

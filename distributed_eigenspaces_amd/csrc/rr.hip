@@ -102,13 +102,10 @@ __device__ __forceinline__ void rr_rot_cs(float app, float aqq, float apq, float
 }
 
 template <int NT>
-__global__ __launch_bounds__(NT) void rr_small_kernel(const float* __restrict__ Cg, int p,
-                                                      float* __restrict__ Wout,
-                                                      float* __restrict__ lam_out,
-                                                      float* __restrict__ cs_out,
-                                                      float* __restrict__ qs_out,
-                                                      int* __restrict__ info, int max_jsweeps,
-                                                      float jrel) {
+__device__ __forceinline__ void rr_small_body(const float* __restrict__ Cg, int p,
+                                              float* __restrict__ Wout, float* __restrict__ lam_out,
+                                              float* __restrict__ cs_out, float* __restrict__ qs_out,
+                                              int* __restrict__ info, int max_jsweeps, float jrel) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int pp = p * p;
   const int half = p >> 1;
@@ -471,6 +468,35 @@ __global__ __launch_bounds__(NT) void rr_small_kernel(const float* __restrict__ 
   stamp(8);
 }
 
+template <int NT>
+__global__ __launch_bounds__(NT) void rr_small_kernel(const float* __restrict__ Cg, int p,
+                                                      float* __restrict__ Wout,
+                                                      float* __restrict__ lam_out,
+                                                      float* __restrict__ cs_out,
+                                                      float* __restrict__ qs_out,
+                                                      int* __restrict__ info, int max_jsweeps,
+                                                      float jrel) {
+  rr_small_body<NT>(Cg, p, Wout, lam_out, cs_out, qs_out, info, max_jsweeps, jrel);
+}
+
+// Up to kRRBatch independent small solves in one launch, one workgroup each (the
+// batched worker solves: W problems' Rayleigh-Ritz steps side by side on W CUs).
+struct RRBatchArgs {
+  const float* C[kRRBatch];
+  float* W[kRRBatch];
+  float* lam[kRRBatch];
+  float* cs[kRRBatch];
+  float* qs[kRRBatch];
+  int* info[kRRBatch];
+  int max_jsweeps[kRRBatch];
+};
+
+template <int NT>
+__global__ __launch_bounds__(NT) void rr_small_batch_kernel(RRBatchArgs a, int p, float jrel) {
+  const int i = blockIdx.x;
+  rr_small_body<NT>(a.C[i], p, a.W[i], a.lam[i], a.cs[i], a.qs[i], a.info[i], a.max_jsweeps[i], jrel);
+}
+
 __global__ __launch_bounds__(256) void rr_update_kernel(float* __restrict__ Z, int64_t d, int p,
                                                         int k, const float* __restrict__ W,
                                                         const float* __restrict__ lam,
@@ -770,6 +796,32 @@ int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream, int max_jswee
   hipLaunchKernelGGL(rr_small_kernel<RT>, dim3(1), dim3(RT), shm, stream, b.C, p, b.W, b.lam, b.cs,
                      b.qs, b.info, max_jsweeps, jrel);
   DEIG_HIP_CHECK(hipGetLastError());
+  return DEIG_OK;
+}
+
+int rr_small_batch_launch(const RRBuffers* const* bs, const int* max_jsweeps, int n, int p,
+                          hipStream_t stream, float jrel) {
+  DEIG_REQUIRE(p >= 4 && p <= 128 && p % 4 == 0, "rr_small: p=%d out of range", p);
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)rr_small_batch_kernel<RT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (int)rr_small_shm(128));
+  DEIG_HIP_CHECK(attr);
+  for (int i0 = 0; i0 < n; i0 += kRRBatch) {
+    const int m = std::min(kRRBatch, n - i0);
+    RRBatchArgs a{};
+    for (int i = 0; i < m; ++i) {
+      const RRBuffers& b = *bs[i0 + i];
+      a.C[i] = b.C;
+      a.W[i] = b.W;
+      a.lam[i] = b.lam;
+      a.cs[i] = b.cs;
+      a.qs[i] = b.qs;
+      a.info[i] = b.info;
+      a.max_jsweeps[i] = max_jsweeps[i0 + i];
+    }
+    hipLaunchKernelGGL(rr_small_batch_kernel<RT>, dim3(m), dim3(RT), rr_small_shm(p), stream, a, p, jrel);
+    DEIG_HIP_CHECK(hipGetLastError());
+  }
   return DEIG_OK;
 }
 

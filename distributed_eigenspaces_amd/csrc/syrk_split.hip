@@ -791,7 +791,10 @@ __global__ __launch_bounds__(NTHR) void syrks_st_kernel(SSched s) {
 //   last two K-tiles wait vmcnt(0).  Stores, atomics and flushes issued in between
 //   only make a counted wait stricter.
 //   WAR: every L part retires its reads (lgkmcnt(0)) before its closing barrier.
-template <int PRIO, int KO = 0>
+// DS (DMA schedule): 0 - per-wave pieces per L part 1 / 5 / 1 / 1 (above); 1 - the
+// B pieces spread over L_1..L_3 (Aq0 + 2 B, Aq1 + B, Aq2 + B: 1 / 3 / 2 / 2), waits
+// 12 / 13 / 13 / 8 (prologue order Aq0 B0 B1 Aq1 B2 Aq2 B3).
+template <int PRIO, int KO = 0, int DS = 0>
 __device__ __forceinline__ void segment_q(const SSched& s, unsigned char* lds, int tile, int64_t k0,
                                           int64_t k1, int slot, bool partial, int pace_j) {
   constexpr int BUF_B = Geo<2>::BUF_B;
@@ -831,12 +834,13 @@ __device__ __forceinline__ void segment_q(const SSched& s, unsigned char* lds, i
     asm volatile("" : "+v"(o));
     dma16(r, o, buf + q * QB + wave * 1024);
   };
-  auto issue_b = [&](int64_t kt, unsigned char* buf) {
+  auto issue_b = [&](int64_t kt, unsigned char* buf, int p0 = 0, int p1 = 4) {
     const i32x4 r = ring_rsrc(kt);
     int o = b_off;
     asm volatile("" : "+v"(o));
 #pragma unroll
-    for (int p = 0; p < 4; ++p) dma16(r, o + p * 1024, buf + BOFF + wave * SLICE_B + p * 1024);
+    for (int p = 0; p < 4; ++p)
+      if (p >= p0 && p < p1) dma16(r, o + p * 1024, buf + BOFF + wave * SLICE_B + p * 1024);
   };
   if (nkt > 0) {
     wait_vm<0>();     // the previous segment's stores / flushes
@@ -845,9 +849,18 @@ __device__ __forceinline__ void segment_q(const SSched& s, unsigned char* lds, i
 #pragma unroll
     for (int q = 0; q < 4; ++q) issue_a(k0, q, lds);
     if (nkt > 1) {
-      issue_b(k0 + 1, lds + BUF_B);
+      if constexpr (DS == 0) {
+        issue_b(k0 + 1, lds + BUF_B);
 #pragma unroll
-      for (int q = 0; q < 3; ++q) issue_a(k0 + 1, q, lds + BUF_B);
+        for (int q = 0; q < 3; ++q) issue_a(k0 + 1, q, lds + BUF_B);
+      } else {
+        issue_a(k0 + 1, 0, lds + BUF_B);
+        issue_b(k0 + 1, lds + BUF_B, 0, 2);
+        issue_a(k0 + 1, 1, lds + BUF_B);
+        issue_b(k0 + 1, lds + BUF_B, 2, 3);
+        issue_a(k0 + 1, 2, lds + BUF_B);
+        issue_b(k0 + 1, lds + BUF_B, 3, 4);
+      }
       wait_vm<7>();  // K-tile k0 landed; K-tile k0 + 1's 7 pieces may fly
     } else {
       wait_vm<0>();
@@ -886,12 +899,17 @@ __device__ __forceinline__ void segment_q(const SSched& s, unsigned char* lds, i
         }
         if (!(KO & 1)) {
           if (q == 0 && has1) issue_a(k0 + t + 1, 3, nxt);
-          if (q == 1 && has2) {
-            issue_b(k0 + t + 2, cur);
-            issue_a(k0 + t + 2, 0, cur);
+          if constexpr (DS == 0) {
+            if (q == 1 && has2) {
+              issue_b(k0 + t + 2, cur);
+              issue_a(k0 + t + 2, 0, cur);
+            }
+            if (q == 2 && has2) issue_a(k0 + t + 2, 1, cur);
+            if (q == 3 && has2) issue_a(k0 + t + 2, 2, cur);
+          } else if (has2 && q >= 1) {
+            issue_a(k0 + t + 2, q - 1, cur);
+            issue_b(k0 + t + 2, cur, q == 1 ? 0 : q, q == 1 ? 2 : q + 1);
           }
-          if (q == 2 && has2) issue_a(k0 + t + 2, 1, cur);
-          if (q == 3 && has2) issue_a(k0 + t + 2, 2, cur);
         }
         if (q == 0 && (!(KO & 2) || t == 0)) {
 #pragma unroll
@@ -906,7 +924,11 @@ __device__ __forceinline__ void segment_q(const SSched& s, unsigned char* lds, i
           alo[m] = *reinterpret_cast<const bf16x8*>(pa + q * QB + (64 + 16 * m) * 16);
         }
         if (has2) {  // the younger-piece counts derived above
-          if (q == 1 || q == 2) wait_vm<14>(); else wait_vm<10>();
+          if constexpr (DS == 0) {
+            if (q == 1 || q == 2) wait_vm<14>(); else wait_vm<10>();
+          } else {
+            if (q == 1 || q == 2) wait_vm<13>(); else if (q == 0) wait_vm<12>(); else wait_vm<8>();
+          }
         } else {
           wait_vm<0>();
         }
@@ -953,7 +975,7 @@ __device__ __forceinline__ void segment_q(const SSched& s, unsigned char* lds, i
   }
 }
 
-template <int PRIO, int KO>
+template <int PRIO, int KO, int DS>
 __global__ __launch_bounds__(NTHR) void syrks_q_kernel(SSched s) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[2 * Geo<2>::BUF_B];
   const int L = xcd_logical(blockIdx.x, s.G);
@@ -974,7 +996,7 @@ __global__ __launch_bounds__(NTHR) void syrks_q_kernel(SSched s) {
       k1 = __builtin_amdgcn_readfirstlane((int)(s.NK * (sg + 1) / s.nseg));
     }
     const int pace_j = (!partial && s.pace_kt > 0) ? (int)(w * (s.NK / s.pace_kt)) : -1;
-    segment_q<PRIO, KO>(s, lds, tile, k0, k1, slot, partial, pace_j);
+    segment_q<PRIO, KO, DS>(s, lds, tile, k0, k1, slot, partial, pace_j);
   }
 }
 
@@ -1187,14 +1209,16 @@ int64_t default_chunk_rows(int64_t n, int64_t d) {
 // 29.0 ms; d = 8192 (config 3 shard) fused 370 ms vs 336 ms.
 // A/B builds (tools/, never the shipped library) fix one with -DDEIG_AB_SYRK_VARIANT=N.
 // Staggered-phase variants are 1PQR0: P phases per K-tile, the next K-tile's
-// pieces over Q of them, R = 1: s_setprio(1) around the MFMA clusters; 2000R0: the
-// quarter-refill ring (segment_q, the default: 315.3 vs 319.6 ms for 14200 at the
-// config-3 shard, interleaved A/B in one process, profiles/r03f_syrk_qring_insplit_ab.log,
-// bit-identical); + 100000 * KO adds the knock-outs (measurement builds only).
+// pieces over Q of them, R = 1: s_setprio(1) around the MFMA clusters; 20DR0: the
+// quarter-refill ring (segment_q) with DMA schedule D.  Default 20100 (config-3 shard,
+// interleaved A/B in one process, bit-identical: 20000 315.3 vs 14200 319.6 ms,
+// profiles/r03f_syrk_qring_insplit_ab.log; 20100 318.5 vs 20000 323.7 ms on another
+// box, profiles/r03l_syrk_dma_schedule_ab.log); + 100000 * KO adds the knock-outs
+// (measurement builds only).
 #ifdef DEIG_AB_SYRK_VARIANT
 constexpr int kSyrkLarge = DEIG_AB_SYRK_VARIANT;
 #else
-constexpr int kSyrkLarge = 20000;
+constexpr int kSyrkLarge = 20100;
 #endif
 int syrk_variant(int64_t d) {
 #ifdef DEIG_AB_SYRK_VARIANT
@@ -1209,7 +1233,8 @@ int syrk_variant(int64_t d) {
 template <int V>
 void launch_split_pass_kernel(int G, hipStream_t stream, const SSched& s) {
   if constexpr (V % 100000 >= 20000) {
-    hipLaunchKernelGGL((syrks_q_kernel<(V / 10) % 10, V / 100000>), dim3(G), dim3(NTHR), 0, stream, s);
+    hipLaunchKernelGGL((syrks_q_kernel<(V / 10) % 10, V / 100000, (V / 100) % 10>), dim3(G), dim3(NTHR), 0,
+                       stream, s);
   } else if constexpr (V >= 10000) {
     hipLaunchKernelGGL((syrks_st_kernel<(V / 1000) % 10, (V / 100) % 10, (V / 10) % 10, V / 100000>), dim3(G),
                        dim3(NTHR), 0, stream, s);

@@ -79,13 +79,19 @@ def _gpu_worker(x: torch.Tensor, k: int, **kw):
 
 class DistributedEigenspaceEstimator:
     def __init__(self, k: int, workers_per_rank: int = 1, server_rank: int = 0, group=None,
-                 worker_fn=None, solver_kw=None, concurrent_workers: bool = False):
+                 worker_fn=None, solver_kw=None, concurrent_workers: bool = False,
+                 batched_workers: bool = True):
         self.k = int(k)
         self.wpr = int(workers_per_rank)
         # concurrent_workers (default GPU worker, W > 1): covariances back to back on
         # the caller's stream, each worker's eigensolve in a my_threading.Slave
         # thread on its own HIP stream, chained by an event (bench.py's c5 mode).
         self.concurrent = bool(concurrent_workers) and worker_fn is None
+        # batched_workers (default GPU worker, W > 1, unless concurrent_workers): the W
+        # covariances back to back, then ONE batched solve (linalg.topk_eigh_batch:
+        # same results as W topk_eigh calls, the small Rayleigh-Ritz solves of all
+        # workers in one launch per step).
+        self.batched = bool(batched_workers) and worker_fn is None and not self.concurrent
         self.server_rank = server_rank
         self.group = group
         self.worker_fn = worker_fn or _gpu_worker
@@ -101,6 +107,11 @@ class DistributedEigenspaceEstimator:
         parts = shard_ranges(X_local.shape[0], self.wpr)
         if self.concurrent and len(parts) > 1 and X_local.is_cuda:
             return self._local_bases_concurrent(X_local, parts)
+        if self.batched and len(parts) > 1 and X_local.is_cuda:
+            Ss = [linalg.sigma_hat(X_local[lo:hi]) for lo, hi in parts]
+            rs = linalg.topk_eigh_batch(Ss, self.k, check_finite=False, **self.solver_kw)
+            return (torch.cat([r.V.t() for r in rs], dim=0).contiguous(), [r.evals for r in rs],
+                    [r.sweeps for r in rs])
         rows, evs, sw = [], [], []
         for lo, hi in parts:
             V, ev, s = self.worker_fn(X_local[lo:hi], self.k, **self.solver_kw)

@@ -21,7 +21,7 @@ import torch
 from . import _lib
 
 __all__ = [
-    "sigma_hat", "topk_eigh", "projavg_topk", "oja_step", "default_subspace",
+    "sigma_hat", "topk_eigh", "topk_eigh_batch", "projavg_topk", "oja_step", "default_subspace",
     "EigResult", "require_device_tensor", "project", "stack_bases", "gemm_skinny",
     "oja_steps", "sym_apply", "sym_power", "sigma_hat_u8", "sigma_hat_shift",
 ]
@@ -382,6 +382,102 @@ def topk_eigh(S: torch.Tensor, k: int, *, p: int | None = None, tol: float = DEF
     if dp != d:
         res.V = res.V[:d].t().contiguous().t()
     return res
+
+
+_batch_streams = threading.local()
+
+
+def _side_streams(device: torch.device, n: int):
+    """n HIP streams of this thread for the batched solver's per-problem work (kept:
+    creating streams per call would cost more than the solves at small d)."""
+    key = device.index
+    pool = getattr(_batch_streams, "pools", None)
+    if pool is None:
+        pool = _batch_streams.pools = {}
+    lst = pool.setdefault(key, [])
+    while len(lst) < n:
+        lst.append(torch.cuda.Stream(device))
+    return lst[:n]
+
+
+def topk_eigh_batch(Ss, k: int, *, p: int | None = None, tol: float = DEFAULT_TOL,
+                    max_sweeps: int = DEFAULT_MAX_SWEEPS, check_finite: bool = True,
+                    opts: "_lib.SolverOpts | None" = None) -> list:
+    """``topk_eigh`` of W same-shape symmetric matrices at once (the logical workers
+    of one GPU, each SlaveNode's top_k_eigenvectors of distributed.py:22-29,
+    :42-53): the same results as W ``topk_eigh`` calls, with the small
+    Rayleigh-Ritz solves of all W problems in one launch per step and each problem's
+    sweeps on its own stream (include/deig.h deig_topk_sym_batch).  Returns a list
+    of EigResult; the work is joined into the current stream."""
+    Ss = [require_device_tensor(S, "topk_eigh_batch", keep_f64=True) for S in Ss]
+    if not Ss:
+        return []
+    S0 = Ss[0]
+    if S0.dim() != 2 or S0.shape[0] != S0.shape[1]:
+        raise ValueError(f"expected square matrices, got {tuple(S0.shape)}")
+    d, dev, dt = S0.shape[0], S0.device, S0.dtype
+    for S in Ss:
+        if S.shape != S0.shape or S.device != dev or S.dtype != dt:
+            raise ValueError("topk_eigh_batch: every matrix must have the same shape, dtype, device")
+        if check_finite and not bool(torch.isfinite(S).all()):
+            raise ValueError("array must not contain infs or NaNs")
+    k = int(k)
+    if not 1 <= k <= d:
+        raise ValueError(f"k={k} out of range [1, {d}]")
+    dp = _pad_dim(d)
+    if not p:
+        dp = max(dp, default_subspace(max(dp, (min(k, MAX_P) + 15) // 16 * 16), k))
+    align = 32 if dt == torch.float64 else 16
+    lds = dp
+    mats = []
+    for S in Ss:
+        if dp != d or S.stride(1) != 1 or S.stride(0) != Ss[0].stride(0) or S.stride(0) % 4 \
+                or S.data_ptr() % align:
+            Sp = torch.zeros((dp, dp), dtype=dt, device=dev)
+            Sp[:d, :d] = S
+            S = Sp
+        mats.append(S)
+    lds = mats[0].stride(0)
+    if any(S.stride(0) != lds for S in mats):
+        mats = [S if S.stride(0) == dp else S.contiguous() for S in mats]
+        lds = dp
+    W = len(mats)
+    pp = int(p) if p else default_subspace(dp, k)
+    stype = _lib.DEIG_F64 if dt == torch.float64 else _lib.DEIG_F32
+    o = opts if opts is not None else _lib.solver_opts()
+    Vs = [_colmajor(dp, k, dev) for _ in range(W)]
+    evs = [torch.empty(k, dtype=torch.float32, device=dev) for _ in range(W)]
+    sweeps = (ctypes.c_int * W)()
+    resid = (ctypes.c_float * W)()
+    vp = ctypes.c_void_p
+    S_arr = (vp * W)(*[S.data_ptr() for S in mats])
+    V_arr = (vp * W)(*[V.data_ptr() for V in Vs])
+    E_arr = (vp * W)(*[e.data_ptr() for e in evs])
+    cur = torch.cuda.current_stream(dev)
+    side = _side_streams(dev, W)
+    for s in side:  # every problem's stream starts behind the caller's stream
+        s.wait_stream(cur)
+    st_arr = (vp * W)(*[s.cuda_stream for s in side])
+    L = _lib.lib()
+    with torch.cuda.device(dev):
+        nbytes = L.deig_topk_batch_workspace(W, dp, k, pp, stype, ctypes.byref(o))
+        ws = _workspace(dev, nbytes)
+        rc = L.deig_topk_sym_batch(W, S_arr, stype, dp, lds, k, pp, int(max_sweeps), ctypes.c_float(tol),
+                                   V_arr, dp, E_arr, sweeps, resid, ctypes.byref(o), ws.data_ptr(),
+                                   nbytes, st_arr, cur.cuda_stream)
+    for t in mats + Vs + evs:  # used on the side streams
+        for s in side:
+            t.record_stream(s)
+    _lib.check(rc, "deig_topk_sym_batch")
+    conv = rc == _lib.DEIG_OK
+    if not conv:
+        warnings.warn(f"deig_topk_sym_batch: {_lib.last_error()}", _lib.NotConvergedWarning, stacklevel=2)
+    out = []
+    for i in range(W):
+        V = Vs[i] if dp == d else Vs[i][:d].t().contiguous().t()
+        out.append(EigResult(evals=evs[i], V=V, sweeps=int(sweeps[i]), resid=float(resid[i]),
+                             converged=conv and float(resid[i]) <= max(float(tol), 0.0) * 4 + 2e-6))
+    return out
 
 
 def stack_bases(bases) -> torch.Tensor:

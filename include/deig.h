@@ -247,6 +247,26 @@ int deig_projavg_topk_f32(const float* Wt, int64_t d, int64_t mk, int64_t ldw,
                           const float* Q0, int k0, int64_t ldq0, float* V, int64_t ldv,
                           float* evals, int* sweeps_out, float* resid_out, void* ws,
                           size_t ws_bytes, void* stream);
+/* W independent top-k problems (the logical workers of one GPU: same d, k, p and
+ * element type; S[i] row-major with leading dimension lds, 16-byte aligned),
+ * advanced in lockstep: equivalent to W deig_topk_sym_ex calls with the same
+ * options (same kernels, same decisions; V[i] column-major with ldv, evals[i]
+ * ascending, sweeps_out[i] / resid_out[i] as there), but the small Rayleigh-Ritz
+ * solves of all problems run in one launch per step (one workgroup each) instead
+ * of W streams contending for the hardware queues.  streams[i]: problem i's stream
+ * for its sweeps and updates (NULL array or entries: `stream`); the batched small
+ * solves run on `stream`, and on return every problem's work has been joined into
+ * `stream`.  Workspace: deig_topk_batch_workspace(W, ...) bytes.  Returns the
+ * first error; DEIG_NOT_CONVERGED if any problem stopped above tol.
+ * Replaces W concurrent Node.top_k_eigenvectors calls (distributed.py:22-29, one
+ * per SlaveNode shard :42-53). */
+size_t deig_topk_batch_workspace(int W, int64_t d, int k, int p, int stype,
+                                 const deig_solver_opts* opts);
+int deig_topk_sym_batch(int W, const void* const* S, int stype, int64_t d, int64_t lds, int k, int p,
+                        int max_sweeps, float tol, float* const* V, int64_t ldv, float* const* evals,
+                        int* sweeps_out, float* resid_out, const deig_solver_opts* opts, void* ws,
+                        size_t ws_bytes, void* const* streams, void* stream);
+
 size_t deig_projavg_workspace(int64_t d, int64_t mk, int k, int p);
 /* With options (k > 128: block locking with the locked pairs deflated by products
  * with them - the operator stays implicit). */

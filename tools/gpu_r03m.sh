@@ -1,0 +1,28 @@
+#!/bin/bash
+# r03m: threaded batch driver tests + c1/c1g benches; c4 kernel trace
+set -o pipefail
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/r03m
+mkdir -p $OUT
+cd $R
+timeout -k 10 400 python -u -m pytest -m gpu -x -v --timeout 200 --timeout-method thread \
+  tests/test_gpu_batch_solver.py tests/test_gpu_configs.py tests/test_gpu_cifar.py \
+  > $OUT/tests.log 2>&1 || { echo "tests failed"; tail -30 $OUT/tests.log; exit 1; }
+tail -3 $OUT/tests.log
+for c in c1 c1g; do
+  timeout -k 10 300 python3 bench.py --config $c --steps 10 --warmup 3 --no-cpu-baseline > $OUT/bench_$c.json 2> $OUT/bench_$c.err \
+    || { echo "bench $c failed"; tail $OUT/bench_$c.err; exit 1; }
+  python3 -c "import json,sys; r=json.load(open('$OUT/bench_$c.json')); print('$c', r['value'], r['ms_per_step'], r.get('breakdown'))"
+done
+timeout -k 10 300 python3 bench.py --config c1 --steps 10 --warmup 3 --no-cpu-baseline --threaded-workers > $OUT/bench_c1_threaded.json 2> $OUT/bench_c1_threaded.err \
+  && python3 -c "import json; r=json.load(open('$OUT/bench_c1_threaded.json')); print('c1 threaded', r['value'], r['ms_per_step'])"
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c4trace -o p -- \
+  python3 $R/bench.py --config c4 --steps 5 --warmup 2 --no-cpu-baseline > $OUT/bench_c4_rocprof.json 2> $OUT/c4trace.err \
+  || { echo "c4 trace failed"; tail $OUT/c4trace.err; exit 1; }
+python3 -c "
+import csv
+r=list(csv.DictReader(open('$OUT/c4trace/p_kernel_stats.csv')))
+for x in r[:10]: print(x['Name'][:70], x['Calls'], round(float(x['AverageNs'])/1e3,2))
+"
