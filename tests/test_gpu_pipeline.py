@@ -283,3 +283,27 @@ def test_socket_two_process_protocol_gpu(tmp_path, cuda):
         assert ref_cpu.projector_distance(r["worker_V"][i], g["worker_V"][i]) <= P_TOL
     assert ref_cpu.projector_distance(r["server_V"], g["server_V"]) <= P_TOL
     np.testing.assert_allclose(r["server_evals"], g["server_evals"], rtol=EV_TOL)
+
+
+@pytest.mark.parametrize("d,b,k", [(500, 1000, 20), (260, 1040, 5), (96, 4100, 33)])
+def test_oja_steps_ragged_shapes_poisoned_workspace(d, b, k, cuda):
+    """Ragged Oja shapes - d and b not multiples of 32 (the last k-steps of both
+    operand images partly past the data), k not a multiple of 16, a row stride
+    > d - with the cached workspace filled with NaN bit patterns first: every
+    image entry the kernels read must be written (zeros past the data)."""
+    import distributed_eigenspaces_amd as de
+    from distributed_eigenspaces_amd import linalg, synthetic
+    nb, eta = 5, 0.4
+    U = synthetic.planted_basis(d, k, seed=7, device=cuda)
+    Xf = torch.zeros((nb * b, d + 12), dtype=torch.float32, device=cuda)
+    Xf[:, :d] = synthetic.spiked_samples(nb * b, U, seed=8)
+    X = Xf[:, :d]
+    V0 = torch.linalg.qr(torch.randn(d, k, device=cuda, dtype=torch.float64))[0]
+    linalg._workspace(X.device, 64 << 20).fill_(0xFF)
+    V = V0.float().t().contiguous().t()
+    de.oja_steps(X, V, eta, b, orth_every=2)
+    Vg = V.cpu().numpy()
+    assert np.isfinite(Vg).all()
+    np.testing.assert_allclose(Vg.T @ Vg, np.eye(k), atol=1e-5)
+    Vr = ref_cpu.oja_epoch(X.double().cpu().numpy(), V0.cpu().numpy(), eta, b)
+    assert ref_cpu.projector_distance(Vg, Vr) <= P_TOL
