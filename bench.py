@@ -380,6 +380,9 @@ def init_dist(args):
     return world, rank, dev
 
 
+STEP_MS: dict = {}
+
+
 def timed_loop(step, args, world, dev):
     for _ in range(args.warmup):
         step(False)
@@ -388,12 +391,18 @@ def timed_loop(step, args, world, dev):
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     out = None
+    ends = []
     for _ in range(args.steps):
         out = step(True)
+        ends.append(time.perf_counter())  # every step ends with a device sync
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    per = np.diff(np.array([t0] + ends)) * 1e3
+    STEP_MS.update(median=float(np.median(per)), min=float(per.min()), max=float(per.max()),
+                   spread_pct=float((per.max() - per.min()) / np.median(per) * 100),
+                   note="this rank's host wall time per timed step (each ends with a device sync)")
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64,
                          device=dev if args.dist_backend == "nccl" else "cpu")
@@ -411,6 +420,7 @@ def base_line(args, world, elapsed, total, dtype, config):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
+        "step_ms": dict(STEP_MS),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

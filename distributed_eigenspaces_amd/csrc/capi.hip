@@ -1,8 +1,10 @@
 // extern "C" boundary of libdeig.so (declared in include/deig.h) and the host
 // drivers of the two eigensolvers.  No device allocation happens here: all
 // device memory is caller-provided (PyTorch tensors on the Python side).  No
-// process-global mutable state: the error string is thread-local, the per-device
-// CU counts are atomics, solver behaviour comes from the caller's options.
+// process-global mutable state beyond: the error string (thread-local), the per-device
+// CU counts (atomics) and a mutex-protected free list of small pinned host blocks the
+// solvers read their per-cycle status from (HostStatus); solver behaviour comes from
+// the caller's options.
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -163,7 +165,7 @@ SolverWs carve_solver(void* ws, size_t cap, int64_t d, int kb, int k, int p, int
   w.Zt = mk > 0 ? c.take<float>((size_t)mk * p) : nullptr;
   w.T = c.take<float>((size_t)d * p);
   w.Tdef = image ? nullptr : c.take<float>((size_t)k * p);
-  w.rq = mk > 0 ? nullptr : c.take<char>(rq_workspace_bytes(d));
+  w.rq = mk > 0 ? nullptr : c.take<char>(rq_workspace_bytes(d, k));
   size_t sb = skinny_workspace_bytes(2 * p, 2 * p, d);  // Gram
   auto need = [&](int64_t M, int64_t N, int64_t K) {
     const size_t b = skinny_workspace_bytes(M, N, K);
@@ -313,6 +315,64 @@ bool cheb_plan(const float* lam, int k, int p, float resid, float tol, float abo
   return true;
 }
 
+// Per-cycle solver status (residuals, Ritz values, the small solve's Jacobi flag),
+// written by status_kernel straight into pinned, mapped host memory and read after
+// the cycle's stream sync: one small launch instead of three device-to-host copies
+// into pageable memory (each a blit kernel plus a staging round trip that blocks
+// the calling thread; c1: 226 copies per step, profiles/r03s).  Blocks come from a
+// process-wide free list (allocated on demand and kept: hipHostFree synchronises
+// the device, which would serialise the Slave threads' streams).
+struct HostStatus {
+  float res[kMaxP + 1];
+  float lam[kMaxP];
+  int jconv;
+};
+
+__global__ __launch_bounds__(256) void status_kernel(const float* __restrict__ resid, int nres,
+                                                     const float* __restrict__ lam, int pb,
+                                                     const int* __restrict__ info,
+                                                     HostStatus* __restrict__ hs) {
+  const int t = threadIdx.x;
+  if (t < nres) hs->res[t] = resid[t];
+  if (t < pb) hs->lam[t] = lam[t];
+  if (t == 0) hs->jconv = info[3];
+}
+
+class StatusPool {
+ public:
+  int acquire(HostStatus** out) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!free_.empty()) {
+      *out = free_.back();
+      free_.pop_back();
+      return DEIG_OK;
+    }
+    void* p = nullptr;
+    if (hipHostMalloc(&p, sizeof(HostStatus), hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess || !p) {
+      (void)hipGetLastError();
+      return fail(DEIG_EHIP, "solver: pinned status block allocation failed");
+    }
+    memset(p, 0, sizeof(HostStatus));
+    *out = static_cast<HostStatus*>(p);
+    return DEIG_OK;
+  }
+  void release(HostStatus* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    free_.push_back(p);
+  }
+
+ private:
+  std::mutex mu_;
+  std::vector<HostStatus*> free_;
+};
+
+StatusPool& status_pool() {
+  static StatusPool pool;  // C++11 thread-safe initialisation; never destroyed before use ends
+  return pool;
+}
+
 struct Solver {
   Operator op;
   Opts o;
@@ -321,9 +381,10 @@ struct Solver {
   float tol;
   SolverWs w;
   hipStream_t st;
-  float lam_h[kMaxP];
-  float res_h[kMaxP + 1];  // per-column residuals of the last RR (descending Ritz order)
-  int jconv_h = 1;         // the last RR's Jacobi converged (rr.hip info[3])
+  HostStatus* hs = nullptr;  // pinned: the last RR's status (status_kernel)
+  const float* lam_h = nullptr;  // hs->lam: Ritz values of the last RR (descending)
+  const float* res_h = nullptr;  // hs->res: per-column residuals (descending Ritz order)
+  int jconv_h = 1;               // the last RR's Jacobi converged (rr.hip info[3])
   int it = 0;              // sweeps done (all blocks and restarts)
   float last = 3.4e38f;
   bool converged = false;
@@ -463,18 +524,16 @@ struct Solver {
   int cycle_update() {
     int rc;
     if ((rc = rr_update_launch(w.rr, d, pb, kc, Vb, ldv, evb, st))) return rc;
-    jconv_h = 1;
-    DEIG_HIP_CHECK(
-        hipMemcpyAsync(res_h, w.rr.resid, sizeof(float) * (kc + 1), hipMemcpyDeviceToHost, st));
-    DEIG_HIP_CHECK(hipMemcpyAsync(lam_h, w.rr.lam, sizeof(float) * pb, hipMemcpyDeviceToHost, st));
-    if (jcap < 30)
-      DEIG_HIP_CHECK(hipMemcpyAsync(&jconv_h, w.rr.info + 3, sizeof(int), hipMemcpyDeviceToHost, st));
+    hipLaunchKernelGGL(status_kernel, dim3(1), dim3(256), 0, st, w.rr.resid, kc + 1, w.rr.lam, pb,
+                       w.rr.info, hs);
+    DEIG_HIP_CHECK(hipGetLastError());
     return DEIG_OK;
   }
 
   // After the sync: *done = the iteration is over (converged, early exit or stalled).
   int cycle_finish(bool* done) {
     *done = false;
+    jconv_h = jcap < 30 ? hs->jconv : 1;
     last = res_h[kc];
     // Ritz pairs of a capped Jacobi that stopped short are approximate: their
     // residual bounds the error, but the eigenvalues / vectors returned are those
@@ -601,6 +660,11 @@ struct SolveSM {
   State state = BLOCK;
   int rc = DEIG_OK;
 
+  SolveSM() = default;
+  SolveSM(const SolveSM&) = delete;
+  SolveSM& operator=(const SolveSM&) = delete;
+  ~SolveSM() { status_pool().release(sv.hs); }
+
   int init(const Operator& op, int64_t d_, int k_, int p, int max_sweeps, float tol, const float* Q0_,
            int k0_, int64_t ldq0_, float* V_, int64_t ldv_, float* evals_, const Opts& o, void* ws,
            size_t ws_bytes, hipStream_t st) {
@@ -623,6 +687,12 @@ struct SolveSM {
     DEIG_REQUIRE(image || op.implicit || op.stype == DEIG_F32,
                  "solver: a float64 S needs the bf16x6 sweep (DEIG_SWEEP_AUTO)");
     size_t total = 0;
+    if (!sv.hs) {
+      int r = status_pool().acquire(&sv.hs);
+      if (r) return r;
+      sv.lam_h = sv.hs->lam;
+      sv.res_h = sv.hs->res;
+    }
     sv.w = carve_solver(ws, ws_bytes, d, kb, k, pb0, op.implicit ? op.mk : 0, image, &total);
     if (!ws || total > ws_bytes)
       return fail(DEIG_EWORKSPACE, "solver: workspace %zu bytes < required %zu", ws_bytes, total);

@@ -12,6 +12,7 @@ namespace deig {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void lds_void;
 
 // ---------------------------------------------------------------- error handling
@@ -170,7 +171,7 @@ int deflate_orth_launch(float* V, int64_t ldv, int64_t d, int kc, int r, hipStre
 // evals[0..k) -= shift (device).
 int unshift_launch(float* evals, int k, double shift, hipStream_t stream);
 // evals[j] = v_j^T S v_j / v_j^T v_j in double for the k columns of V (S: stype).
-size_t rq_workspace_bytes(int64_t d);
+size_t rq_workspace_bytes(int64_t d, int k);
 int rq_launch(const void* S, int stype, int64_t d, int64_t lds, const float* V, int64_t ldv, int k,
               float* evals, void* ws, hipStream_t stream);
 

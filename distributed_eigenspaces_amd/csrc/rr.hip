@@ -704,67 +704,158 @@ __global__ void unshift_kernel(float* __restrict__ evals, int k, double shift) {
 // The fp32 Rayleigh-Ritz values carry ~1e-7 of the operator's scale (a few ulps of
 // |H| in the small solve); a quotient of a vector with sin(angle) ~ 1e-6 is exact to
 // ~1e-12 of the spread, and it is taken on S itself - unshifted, undeflated.
-// grid (cdiv(d, RQ_R), vector groups of RQ_K); thread = (row tid / 8, 4 vectors).
-constexpr int RQ_R = 32, RQ_L = 64, RQ_K = 32, RQ_GY = 4;
-template <typename T>
-__global__ __launch_bounds__(256) void rq_kernel(const T* __restrict__ S, int64_t lds, int64_t d,
-                                                 const float* __restrict__ V, int64_t ldv, int j0,
-                                                 int k, double* __restrict__ part) {
-  __shared__ double Ss[RQ_R][RQ_L + 1];
-  __shared__ double Vs[RQ_L][RQ_K];
-  __shared__ double red[RQ_R][2 * RQ_K + 1];
-  const int tid = threadIdx.x, i = tid >> 3, jg = tid & 7;
-  const int64_t r0 = (int64_t)blockIdx.x * RQ_R;
-  const int jb = j0 + blockIdx.y * RQ_K;  // first vector of this block
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int64_t l0 = 0; l0 < d; l0 += RQ_L) {
-    for (int e = tid; e < RQ_R * RQ_L; e += 256) {
-      const int rr = e / RQ_L, cc = e - rr * RQ_L;
-      const int64_t row = r0 + rr, col = l0 + cc;
-      Ss[rr][cc] = (row < d && col < d) ? (double)S[row * lds + col] : 0.0;
-    }
-    for (int e = tid; e < RQ_L * RQ_K; e += 256) {
-      const int jj = e / RQ_L, ll = e - jj * RQ_L;
-      const int64_t l = l0 + ll;
-      Vs[ll][jj] = (l < d && jb + jj < k) ? (double)V[(int64_t)(jb + jj) * ldv + l] : 0.0;
-    }
-    __syncthreads();
-#pragma unroll 8
-    for (int ll = 0; ll < RQ_L; ++ll) {
-      const double s = Ss[i][ll];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc[u] = fma(s, Vs[ll][4 * jg + u], acc[u]);
-    }
-    __syncthreads();
-  }
-  const int64_t row = r0 + i;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int j = jb + 4 * jg + u;
-    const double v = (row < d && j < k) ? (double)V[(int64_t)j * ldv + row] : 0.0;
-    red[i][4 * jg + u] = v * acc[u];
-    red[i][RQ_K + 4 * jg + u] = v * v;
-  }
-  __syncthreads();
-  if (tid < 2 * RQ_K) {
-    double s = 0.0;
-    for (int rr = 0; rr < RQ_R; ++rr) s += red[rr][tid];  // fixed order
-    part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 2 * RQ_K + tid] = s;
-  }
+// Products s * v of fp32 values are exact in double; sums are in double, in a fixed
+// order (deterministic).
+//   rq_vd_kernel:   Vd[r][j] = v_j[r] as double (zero for k <= j < kpad = 16 ng);
+//   rq_part_kernel: block (cb, rb) = 1024 columns x RQ_RB rows; lane c of wave w owns
+//                   columns c0 + 256 w + c + 64 u (u < 4, coalesced row reads of S, all
+//                   issued before the first FMA, kept in registers for every group).
+//                   Per group g of RQ_KG = 16 vectors: the block's Vd rows of the group
+//                   go to LDS, acc[u][jj] = sum_r S[r][c_u] Vd[r][16 g + jj] (each row's
+//                   16 values, 8 broadcast ds_read_b128, feed 64 FMAs), then t_jj =
+//                   sum_u acc[u][jj] v_{16g+jj}[c_u] is summed over the block
+//                   (recursive-halving butterflies, the 4 waves in order) into
+//                   part[block][16 g + jj];
+//   rq_finish_kernel: block j sums the parts in block order and v_j^T v_j.
+// One read of S, d^2 x kpad fp64 FMA.  (Earlier versions: 32 rows x all
+// columns per block staged through LDS, 387 us at d = 3072, k = 10 - 3.1 ms of c1's
+// 11.1 ms step, profiles/r03s; one column per lane with the Vd row as scalar loads,
+// 166 us: every row waited on a scalar-cache miss, profiles/r03t.)
+constexpr int RQ_KG = 16;   // vectors per pass
+constexpr int RQ_CPT = 4;   // columns per lane
+constexpr int RQ_RB = 8;    // rows per block (16: sv + acc spilled)
+constexpr int RQ_CB = 4 * 64 * RQ_CPT;  // columns per block
+
+__global__ __launch_bounds__(256) void rq_vd_kernel(const float* __restrict__ V, int64_t ldv,
+                                                    int64_t d, int k, int kpad,
+                                                    double* __restrict__ Vd) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= d * kpad) return;
+  const int64_t r = idx / kpad;
+  const int j = (int)(idx - r * kpad);
+  Vd[idx] = j < k ? (double)V[(int64_t)j * ldv + r] : 0.0;
 }
 
-__global__ __launch_bounds__(256) void rq_finish_kernel(const double* __restrict__ part, int nbx,
-                                                        int j0, int k, float* __restrict__ evals) {
-  const int t = blockIdx.x * 256 + threadIdx.x;  // vector j0 + t
-  if (t >= RQ_GY * RQ_K || j0 + t >= k) return;
-  const int gy = t / RQ_K, jj = t - gy * RQ_K;
-  double q = 0.0, nn = 0.0;
-  for (int b = 0; b < nbx; ++b) {
-    const double* p = part + ((int64_t)gy * nbx + b) * 2 * RQ_K;
-    q += p[jj];
-    nn += p[RQ_K + jj];
+template <typename T>
+__global__ __launch_bounds__(256) void rq_part_kernel(const T* __restrict__ S, int64_t lds, int64_t d,
+                                                      const double* __restrict__ Vd,
+                                                      const float* __restrict__ V, int64_t ldv,
+                                                      int k, int ng, double* __restrict__ part) {
+  constexpr int KG = RQ_KG, LG = 4;
+  const int kpad = KG * ng;
+  __shared__ __attribute__((aligned(16))) double vs[RQ_RB][KG];
+  __shared__ double red[4][KG];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t r0 = (int64_t)blockIdx.y * RQ_RB;
+  const int64_t cw = (int64_t)blockIdx.x * RQ_CB + 256 * wave + lane;
+  // unpredicated loads at clamped in-range addresses (a branch per load otherwise),
+  // out-of-range values zeroed by a select
+  T sv[RQ_RB][RQ_CPT];
+#pragma unroll
+  for (int r = 0; r < RQ_RB; ++r)
+#pragma unroll
+    for (int u = 0; u < RQ_CPT; ++u) {
+      const int64_t c = cw + 64 * u;
+      const int64_t rr = r0 + r < d ? r0 + r : d - 1;
+      const T x = S[rr * lds + (c < d ? c : d - 1)];
+      sv[r][u] = (r0 + r < d && c < d) ? x : T(0);
+    }
+  for (int g = 0; g < ng; ++g) {
+  const int j0 = KG * g;
+  if (g) __syncthreads();  // the last group's vs / red reads are done
+  for (int e = tid; e < RQ_RB * KG; e += 256) {
+    const int rr = e / KG;
+    vs[rr][e - rr * KG] = r0 + rr < d ? Vd[(r0 + rr) * kpad + j0 + (e - rr * KG)] : 0.0;
   }
-  if (nn > 0.0) evals[j0 + t] = (float)(q / nn);
+  __syncthreads();
+  double acc[RQ_CPT][KG];
+#pragma unroll
+  for (int u = 0; u < RQ_CPT; ++u)
+#pragma unroll
+    for (int jj = 0; jj < KG; ++jj) acc[u][jj] = 0.0;
+#pragma unroll
+  for (int r = 0; r < RQ_RB; ++r) {
+    double vv[KG];
+#pragma unroll
+    for (int jj = 0; jj < KG; jj += 2) {
+      const f64x2 w = *reinterpret_cast<const f64x2*>(&vs[r][jj]);
+      vv[jj] = w[0];
+      vv[jj + 1] = w[1];
+    }
+#pragma unroll
+    for (int u = 0; u < RQ_CPT; ++u) {
+      const double sd = (double)sv[r][u];
+#pragma unroll
+      for (int jj = 0; jj < KG; ++jj) acc[u][jj] = fma(sd, vv[jj], acc[u][jj]);
+    }
+  }
+  // (the epilogue's 64 V loads stay below the FMAs: hoisted, they spilled)
+  __builtin_amdgcn_sched_barrier(0);
+  double t[KG];
+#pragma unroll
+  for (int jj = 0; jj < KG; ++jj) t[jj] = 0.0;
+#pragma unroll
+  for (int u = 0; u < RQ_CPT; ++u) {
+    const int64_t c = cw + 64 * u;
+    const float* vc = V + (c < d ? c : d - 1);
+#pragma unroll
+    for (int jj = 0; jj < KG; ++jj) {
+      const int j = j0 + jj;
+      const float x = vc[(int64_t)(j < k ? j : k - 1) * ldv];
+      t[jj] = fma(acc[u][jj], (c < d && j < k) ? (double)x : 0.0, t[jj]);
+    }
+  }
+  // recursive halving over the wave: at step s (mask 32 >> s) a lane keeps the upper
+  // half of its values if its mask bit is set, and adds its partner's copy of them
+#pragma unroll
+  for (int st = 0; st < LG; ++st) {
+    const int m = 32 >> st, h = KG >> (st + 1);
+    const bool up = (lane & m) != 0;
+#pragma unroll
+    for (int i = 0; i < h; ++i) {
+      const double send = up ? t[i] : t[i + h];
+      const double keep = up ? t[i + h] : t[i];
+      t[i] = keep + __shfl_xor(send, m, 64);
+    }
+  }
+  // lane holds the wave sum of vector lane >> 2 over its group of 4 lanes; fold the
+  // group (commutative adds: every lane of it ends equal)
+  t[0] += __shfl_xor(t[0], 2, 64);
+  t[0] += __shfl_xor(t[0], 1, 64);
+  if ((lane & 3) == 0) red[wave][lane >> 2] = t[0];
+  __syncthreads();
+  if (tid < KG)
+    part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kpad + j0 + tid] =
+        ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+  }  // groups
+}
+
+// block j: q = sum over the nblk parts (thread-strided, then a fixed LDS tree),
+// n = v^T v the same way; evals[j] = q / n.
+__global__ __launch_bounds__(256) void rq_finish_kernel(const double* __restrict__ part, int64_t nblk,
+                                                        int kpad, const float* __restrict__ V,
+                                                        int64_t ldv, int64_t d,
+                                                        float* __restrict__ evals) {
+  __shared__ double rq[256], rn[256];
+  const int tid = threadIdx.x, j = blockIdx.x;
+  double q = 0.0, nn = 0.0;
+  for (int64_t b = tid; b < nblk; b += 256) q += part[b * kpad + j];
+  const float* v = V + (int64_t)j * ldv;
+  for (int64_t r = tid; r < d; r += 256) {
+    const double x = (double)v[r];
+    nn = fma(x, x, nn);
+  }
+  rq[tid] = q;
+  rn[tid] = nn;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (tid < w) {
+      rq[tid] += rq[tid + w];
+      rn[tid] += rn[tid + w];
+    }
+    __syncthreads();
+  }
+  if (tid == 0 && rn[0] > 0.0) evals[j] = (float)(rq[0] / rn[0]);
 }
 
 size_t rr_small_shm(int p) {
@@ -848,27 +939,32 @@ int deflate_orth_launch(float* V, int64_t ldv, int64_t d, int kc, int r, hipStre
   return DEIG_OK;
 }
 
-size_t rq_workspace_bytes(int64_t d) {
-  return (size_t)cdiv(d, RQ_R) * RQ_GY * 2 * RQ_K * sizeof(double);
+size_t rq_workspace_bytes(int64_t d, int k) {
+  const int64_t nblk = cdiv(d, RQ_CB) * cdiv(d, RQ_RB);
+  return (size_t)(d + nblk) * cdiv(k, RQ_KG) * RQ_KG * sizeof(double);
 }
 
 int rq_launch(const void* S, int stype, int64_t d, int64_t lds, const float* V, int64_t ldv, int k,
               float* evals, void* ws, hipStream_t stream) {
-  double* part = static_cast<double*>(ws);
-  const int nbx = (int)cdiv(d, RQ_R);
-  for (int j0 = 0; j0 < k; j0 += RQ_GY * RQ_K) {
-    const int gy = (int)std::min<int64_t>(RQ_GY, cdiv(k - j0, RQ_K));
-    const dim3 grid((unsigned)nbx, (unsigned)gy);
-    if (stype == DEIG_F64)
-      hipLaunchKernelGGL(rq_kernel<double>, grid, dim3(256), 0, stream,
-                         static_cast<const double*>(S), lds, d, V, ldv, j0, k, part);
-    else
-      hipLaunchKernelGGL(rq_kernel<float>, grid, dim3(256), 0, stream,
-                         static_cast<const float*>(S), lds, d, V, ldv, j0, k, part);
-    DEIG_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(rq_finish_kernel, dim3(1), dim3(256), 0, stream, part, nbx, j0, k, evals);
-    DEIG_HIP_CHECK(hipGetLastError());
-  }
+  DEIG_REQUIRE(k >= 1 && k <= d, "rq: need 1 <= k <= d (k=%d)", k);
+  const int ng = (int)cdiv(k, RQ_KG), kpad = RQ_KG * ng;
+  double* Vd = static_cast<double*>(ws);
+  double* part = Vd + d * kpad;
+  const dim3 grid((unsigned)cdiv(d, RQ_CB), (unsigned)cdiv(d, RQ_RB));
+  const int64_t nblk = (int64_t)grid.x * grid.y;
+  hipLaunchKernelGGL(rq_vd_kernel, dim3((unsigned)cdiv(d * kpad, 256)), dim3(256), 0, stream, V, ldv,
+                     d, k, kpad, Vd);
+  DEIG_HIP_CHECK(hipGetLastError());
+  if (stype == DEIG_F64)
+    hipLaunchKernelGGL(rq_part_kernel<double>, grid, dim3(256), 0, stream,
+                       static_cast<const double*>(S), lds, d, Vd, V, ldv, k, ng, part);
+  else
+    hipLaunchKernelGGL(rq_part_kernel<float>, grid, dim3(256), 0, stream,
+                       static_cast<const float*>(S), lds, d, Vd, V, ldv, k, ng, part);
+  DEIG_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(rq_finish_kernel, dim3((unsigned)k), dim3(256), 0, stream, part, nblk, kpad, V,
+                     ldv, d, evals);
+  DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }
 

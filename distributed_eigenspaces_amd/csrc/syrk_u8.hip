@@ -36,7 +36,7 @@ constexpr int KB = 64;        // rows per K-step (one MFMA 16x16x64 depth)
 constexpr int TB = 128;       // output tile edge (features)
 constexpr int FPAD = 128;     // features padded to a multiple of this
 constexpr int SYRK_THR = 256;  // 4 waves, 2 x 2 wave tiles of 64 x 64
-constexpr int PREP_THR = 64;   // prep: one wave, 4 features per lane
+constexpr int PREP_THR = 256;  // prep: 4 waves (one 16-row group each), 4 features per lane
 constexpr int MAX_SEG_KB = 1024;  // <= 65536 rows per item: int32 accumulators cannot overflow
 constexpr int PREP_YB = 128;
 
@@ -63,10 +63,12 @@ __device__ __forceinline__ void tr4(const uint32_t r[4], uint32_t out[4]) {
 
 __device__ __forceinline__ int sbyte(uint32_t v, int u) { return (int)(int8_t)(v >> (8 * u)); }
 
-// grid (fpad / 256, YB): lane owns features f .. f + 3 (f = 256 bx + 4 lane) and
-// walks row blocks kb = by, by + YB, ...; per 16-row group it loads one dword
-// (raw) or three (gray) per row, forms the int8 plane values, transposes 4 x 4
-// byte blocks and writes 16 B per feature and plane (coalesced across lanes).
+// grid (fpad / 256, YB), 4 waves: lane owns features f .. f + 3 (f = 256 bx + 4 lane)
+// and wave g the 16-row group g of row blocks kb = by, by + YB, ...; per group it
+// loads one dword (raw) or three (gray) per row, forms the int8 plane values,
+// transposes 4 x 4 byte blocks and writes 16 B per feature and plane (coalesced
+// across lanes).  The 4 waves' column sums meet in LDS: one atomic per feature and
+// block.  (One wave walking all 4 groups: 44 us for a c1 worker shard, r03s.)
 template <int MODE>
 __global__ __launch_bounds__(PREP_THR) void u8_prep_kernel(const uint8_t* __restrict__ X,
                                                            int64_t n, int64_t ldx, int d,
@@ -74,11 +76,13 @@ __global__ __launch_bounds__(PREP_THR) void u8_prep_kernel(const uint8_t* __rest
                                                            uint8_t* __restrict__ img,
                                                            unsigned long long* __restrict__ colsum) {
   constexpr int NP = MODE == DEIG_U8_GRAY3 ? 3 : 1;
-  const int f = blockIdx.x * 256 + threadIdx.x * 4;
+  __shared__ long long cs[4][256];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int f = blockIdx.x * 256 + lane * 4;
   const bool fin = f < d;  // d % 4 == 0: the 4 features are all in or all out
   int csum[4] = {0, 0, 0, 0};
   for (int64_t kb = blockIdx.y; kb < nkb; kb += gridDim.y) {
-    for (int g = 0; g < 4; ++g) {
+    {
       uint32_t rows[NP][16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -119,7 +123,7 @@ __global__ __launch_bounds__(PREP_THR) void u8_prep_kernel(const uint8_t* __rest
           rows[NP > 2 ? 2 : 0][r] = pw;
         }
       }
-      if (f >= fpad) continue;
+      if (f >= fpad) continue;  // (uniform per wave: fpad % 256 == 0 or the last lanes)
 #pragma unroll
       for (int pl = 0; pl < NP; ++pl) {
         uint32_t col[4][4];  // [feature u][dword q]
@@ -137,10 +141,14 @@ __global__ __launch_bounds__(PREP_THR) void u8_prep_kernel(const uint8_t* __rest
       }
     }
   }
-  if (fin) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      atomicAdd(colsum + f + u, (unsigned long long)(long long)csum[u]);
+  for (int u = 0; u < 4; ++u) cs[g][4 * lane + u] = csum[u];
+  __syncthreads();
+  const int t = threadIdx.x;  // feature 256 bx + t
+  const int64_t ft = (int64_t)blockIdx.x * 256 + t;
+  if (ft < d) {
+    const long long v = ((cs[0][t] + cs[1][t]) + cs[2][t]) + cs[3][t];
+    atomicAdd(colsum + ft, (unsigned long long)v);
   }
 }
 
@@ -150,6 +158,12 @@ struct U8Sched {
   const int* order;       // lower tile list: ti | tj << 16
   int64_t nkb, fpad;
   int T, nseg;
+  // direct epilogue (raw mode, one K segment): S written from the accumulators
+  const unsigned long long* colsum;
+  int64_t d, n, div, lds, lds64;
+  double alpha;
+  float* S;
+  double* S64;
 };
 
 // One item = (plane, lower tile, K segment).  LDS: 2 stages x (A panel, B panel),
@@ -157,6 +171,12 @@ struct U8Sched {
 // image's [kb][g][f0 .. f0+127] runs.  Wave (wi, wj) owns rows 64 wi.. and columns
 // 64 wj.. of the tile: 4 x 4 MFMA blocks, lane l reads the A fragment of feature
 // 16 a + (l & 15), row group l >> 4 (16 consecutive rows = 16 bytes).
+// DIRECT (raw mode, the whole K range in one item: n <= 65536 rows, so the int32
+// accumulators are the exact sums): the epilogue adds the mean terms in int64,
+// scales once in double (as u8_finalize_kernel) and stores S[i][j] and S[j][i] -
+// no int64 image, no memset, no atomics, no finalize pass (c1 worker shard: the
+// image path's memset + atomics + finalize were most of its 0.30 ms, r03s).
+template <bool DIRECT>
 __global__ __launch_bounds__(SYRK_THR) void u8_syrk_kernel(U8Sched s) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[2][2][4 * TB * 16];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -198,20 +218,26 @@ __global__ __launch_bounds__(SYRK_THR) void u8_syrk_kernel(U8Sched s) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = i32x4{0, 0, 0, 0};
 
-  u32x4 ra[2], rb[2];
-  if (k0 < k1) {
-    load(k0, ra, rb);
-    put(0, ra, rb);
-  }
+  if (k0 >= k1) return;  // (whole block: an empty K segment adds nothing)
+  // K loop: LDS double buffer fed from a PF-deep register ring - the loads of k-step
+  // kk + PF are issued while kk's MFMAs run, so each load has PF - 1 steps to land
+  // (one step ahead, a c1 worker shard took 149 us: every step waited out a global
+  // load latency).  Loads are unpredicated (clamped to the last k-step) so that the
+  // compiler's counted waits keep the ring in flight; PF even: stage = u & 1.
+  constexpr int PF = 4;
+  u32x4 ra[PF][2], rb[PF][2];
+  auto clampk = [&](int64_t kb) { return kb < k1 ? kb : k1 - 1; };
+#pragma unroll
+  for (int u = 0; u < PF; ++u) load(clampk(k0 + u), ra[u], rb[u]);
+  put(0, ra[0], rb[0]);
   __syncthreads();
-  int st = 0;
-  for (int64_t kb = k0; kb < k1; ++kb) {
-    const bool more = kb + 1 < k1;
-    if (more) load(kb + 1, ra, rb);  // in flight while this stage's MFMAs run
+  const int g = lane >> 4, c = lane & 15;
+  auto body = [&](int64_t kk, int u) {
+    load(clampk(kk + PF), ra[u], rb[u]);  // slot u's k-step is already in LDS
+    const int st = u & 1;
     if (active) {
       const uint8_t* pa = &lds[st][0][0];
       const uint8_t* pb = diag ? pa : &lds[st][1][0];
-      const int g = lane >> 4, c = lane & 15;
       i32x4 fa[4], fb[4];
 #pragma unroll
       for (int a = 0; a < 4; ++a)
@@ -225,12 +251,51 @@ __global__ __launch_bounds__(SYRK_THR) void u8_syrk_kernel(U8Sched s) {
         for (int b = 0; b < 4; ++b)
           acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
     }
-    if (more) put(st ^ 1, ra, rb);
+    put(st ^ 1, ra[(u + 1) % PF], rb[(u + 1) % PF]);  // k-step kk + 1 (a clamped copy past k1)
     __syncthreads();
-    st ^= 1;
+  };
+  int64_t kb = k0;
+  for (; kb + PF <= k1; kb += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) body(kb + u, u);
   }
-  if (!active || k0 >= k1) return;
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (kb + u < k1) body(kb + u, u);
+  if (!active) return;
   // C/D map (gfx950, dtype independent): column = lane & 15, row = 4 (lane >> 4) + reg
+  if constexpr (DIRECT) {
+    long long cjv[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int64_t j = j0 + 64 * wj + 16 * b + (lane & 15);
+      cjv[b] = j < s.d ? (long long)s.colsum[j] : 0ll;
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t i = i0 + 64 * wi + 16 * a + 4 * (lane >> 4) + r;
+        if (i >= s.d) continue;
+        const long long ci = (long long)s.colsum[i];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int64_t j = j0 + 64 * wj + 16 * b + (lane & 15);
+          if (j >= s.d || (diag && j > i)) continue;
+          const long long v64 = (long long)acc[a][b][r] + 128ll * (ci + cjv[b]) + 16384ll * s.n;
+          const double v = s.div > 0 ? (double)v64 / (double)s.div : s.alpha * (double)v64;
+          if (s.S) {
+            s.S[i * s.lds + j] = (float)v;
+            s.S[j * s.lds + i] = (float)v;
+          }
+          if (s.S64) {
+            s.S64[i * s.lds64 + j] = v;
+            s.S64[j * s.lds64 + i] = v;
+          }
+        }
+      }
+    return;
+  }
   unsigned long long* Gp = s.G + (int64_t)plane * s.fpad * s.fpad;
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -344,8 +409,13 @@ int syrk_u8_launch(const uint8_t* X, int64_t n, int64_t d, int64_t ldx, int mode
   unsigned long long* col = reinterpret_cast<unsigned long long*>(base + L.off_col);
   unsigned long long* G = reinterpret_cast<unsigned long long*>(base + L.off_G);
   uint8_t* img = reinterpret_cast<uint8_t*>(base + L.off_img);
+  const int G_ = num_cus();
+  // direct epilogue: raw mode, one K segment (int32 exact), enough tiles to fill half
+  // the chip (config 1: 300 tiles of a 3072-feature worker shard)
+  const bool direct = mode == DEIG_U8_RAW && L.nkb <= MAX_SEG_KB && 2 * L.T >= G_;
   DEIG_HIP_CHECK(hipMemsetAsync(col, 0, sizeof(unsigned long long) * L.fpad, stream));
-  DEIG_HIP_CHECK(hipMemsetAsync(G, 0, sizeof(unsigned long long) * L.planes * L.fpad * L.fpad, stream));
+  if (!direct)
+    DEIG_HIP_CHECK(hipMemsetAsync(G, 0, sizeof(unsigned long long) * L.planes * L.fpad * L.fpad, stream));
   hipLaunchKernelGGL(u8_tile_order_kernel, dim3(1), dim3(64), 0, stream, (int)L.nt, order);
   DEIG_HIP_CHECK(hipGetLastError());
   const int yb = (int)(L.nkb < PREP_YB ? L.nkb : PREP_YB);
@@ -359,11 +429,10 @@ int syrk_u8_launch(const uint8_t* X, int64_t n, int64_t d, int64_t ldx, int mode
   DEIG_HIP_CHECK(hipGetLastError());
   // K segments: enough items to fill the chip twice over, each <= MAX_SEG_KB row
   // blocks (int32 accumulators) and >= 4 (amortise the staging prologue).
-  const int G_ = num_cus();
-  int64_t nseg = cdiv(2 * G_, L.T * L.planes);
+  int64_t nseg = direct ? 1 : cdiv(2 * G_, L.T * L.planes);
   const int64_t min_seg = cdiv(L.nkb, MAX_SEG_KB);
   if (nseg < min_seg) nseg = min_seg;
-  if (nseg > cdiv(L.nkb, 4)) nseg = cdiv(L.nkb, 4) > min_seg ? cdiv(L.nkb, 4) : min_seg;
+  if (!direct && nseg > cdiv(L.nkb, 4)) nseg = cdiv(L.nkb, 4) > min_seg ? cdiv(L.nkb, 4) : min_seg;
   if (nseg < 1) nseg = 1;
   U8Sched s;
   s.img = img;
@@ -373,11 +442,25 @@ int syrk_u8_launch(const uint8_t* X, int64_t n, int64_t d, int64_t ldx, int mode
   s.fpad = L.fpad;
   s.T = (int)L.T;
   s.nseg = (int)nseg;
-  hipLaunchKernelGGL(u8_syrk_kernel, dim3((unsigned)(L.T * nseg), (unsigned)L.planes),
+  const int64_t div = (alpha == 1.0 / (double)n && n < (int64_t(1) << 48)) ? n : 0;
+  s.colsum = col;
+  s.d = d;
+  s.n = n;
+  s.div = div;
+  s.alpha = alpha;
+  s.S = S;
+  s.lds = lds;
+  s.S64 = S64;
+  s.lds64 = lds64;
+  if (direct) {
+    hipLaunchKernelGGL(u8_syrk_kernel<true>, dim3((unsigned)L.T, 1u), dim3(SYRK_THR), 0, stream, s);
+    DEIG_HIP_CHECK(hipGetLastError());
+    return DEIG_OK;
+  }
+  hipLaunchKernelGGL(u8_syrk_kernel<false>, dim3((unsigned)(L.T * nseg), (unsigned)L.planes),
                      dim3(SYRK_THR), 0, stream, s);
   DEIG_HIP_CHECK(hipGetLastError());
   const dim3 fg((unsigned)cdiv(d * d, 256));
-  const int64_t div = (alpha == 1.0 / (double)n && n < (int64_t(1) << 48)) ? n : 0;
   if (mode == DEIG_U8_RAW)
     hipLaunchKernelGGL(u8_finalize_kernel<DEIG_U8_RAW>, fg, dim3(256), 0, stream, G, col, L.fpad, d,
                        n, alpha, div, S, lds, S64, lds64);

@@ -89,3 +89,37 @@ def test_compute_sigma_hat_dropin_uint8(cuda):
     assert isinstance(S, np.ndarray) and S.dtype == np.float64
     ref = ref_cpu.sigma_hat(X.astype(np.float64))
     np.testing.assert_allclose(S, ref, rtol=1.01 * ULP32, atol=0)
+
+
+@pytest.mark.parametrize("n,d", [(65536, 2052), (65537, 2052), (3000, 2048)])
+def test_direct_epilogue_edges(n, d, cuda):
+    """Raw shards whose whole K range fits one int32 item (n <= 65536) and whose
+    tiles fill half the chip take the direct epilogue (S stored from the
+    accumulators, no int64 image): the largest such n, one row more (image path),
+    a ragged d (last tile partly past d) and extreme columns.  Reference: exact int64
+    sums on a column subset that spans the first and last tiles (one rounding for
+    /n), the full matrix within 1e-15 of a float64 GEMM (hipBLAS's float64 GEMM is
+    not exact on integer data at these sizes: tools/diag_u8_exact.py, r03v)."""
+    import distributed_eigenspaces_amd as de
+    rng = np.random.default_rng(n + d)
+    Xh = rng.integers(0, 256, (n, d), dtype=np.uint8)
+    Xh[:, 0] = 255
+    Xh[:, 1] = 0
+    Xh[::2, d - 1] = 255
+    X = torch.from_numpy(Xh).to(cuda)
+    S64 = de.linalg.sigma_hat_u8(X, dtype=torch.float64)
+    S32 = de.linalg.sigma_hat_u8(X)
+    cols = np.r_[0:40, 1000:1024, d - 40:d]
+    Xi = Xh[:, cols].astype(np.int64)
+    exact = (Xi.T @ Xi).astype(np.float64) / n
+    np.testing.assert_array_equal(S64.cpu().numpy()[np.ix_(cols, cols)], exact)
+    np.testing.assert_array_equal(S32.cpu().numpy()[np.ix_(cols, cols)], exact.astype(np.float32))
+    assert torch.equal(S64, S64.t()) and torch.equal(S32, S32.t())
+    Xf = X.double()
+    torch.testing.assert_close(S64, (Xf.t() @ Xf) / n, rtol=1e-15, atol=0)
+    # alpha = 1 (no /n) on a row-strided view of a wider array
+    m = min(n, 3000)
+    Wd = rng.integers(0, 256, (m, d + 12), dtype=np.uint8)
+    S1 = de.linalg.sigma_hat_u8(torch.from_numpy(Wd).to(cuda)[:, :d], alpha=1.0, dtype=torch.float64)
+    Wi = Wd[:, cols].astype(np.int64)
+    np.testing.assert_array_equal(S1.cpu().numpy()[np.ix_(cols, cols)], (Wi.T @ Wi).astype(np.float64))
