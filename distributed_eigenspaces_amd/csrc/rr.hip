@@ -707,14 +707,14 @@ __global__ void unshift_kernel(float* __restrict__ evals, int k, double shift) {
 // Products s * v of fp32 values are exact in double; sums are in double, in a fixed
 // order (deterministic).
 //   rq_vd_kernel:   Vd[r][j] = v_j[r] as double (zero for k <= j < kpad = 16 ng);
-//   rq_part_kernel: block (cb, rb) = 1024 columns x RQ_RB rows; lane c of wave w owns
-//                   columns c0 + 256 w + c + 64 u (u < 4, coalesced row reads of S, all
+//   rq_part_kernel: block (cb, rb) = 512 columns x RQ_RB rows; lane c of wave w owns
+//                   columns c0 + 128 w + c + 64 u (u < 2, coalesced row reads of S, all
 //                   issued before the first FMA, kept in registers for every group).
 //                   Per group g of RQ_KG = 16 vectors: the block's Vd rows of the group
 //                   go to LDS, acc[u][jj] = sum_r S[r][c_u] Vd[r][16 g + jj] (each row's
-//                   16 values, 8 broadcast ds_read_b128, feed 64 FMAs), then t_jj =
+//                   16 values, 8 broadcast ds_read_b128, feed 32 FMAs), then t_jj =
 //                   sum_u acc[u][jj] v_{16g+jj}[c_u] is summed over the block
-//                   (recursive-halving butterflies, the 4 waves in order) into
+//                   (an LDS transpose per wave, the 4 waves in order) into
 //                   part[block][16 g + jj];
 //   rq_finish_kernel: block j sums the parts in block order and v_j^T v_j.
 // One read of S, d^2 x kpad fp64 FMA.  (Earlier versions: 32 rows x all
@@ -722,8 +722,8 @@ __global__ void unshift_kernel(float* __restrict__ evals, int k, double shift) {
 // 11.1 ms step, profiles/r03s; one column per lane with the Vd row as scalar loads,
 // 166 us: every row waited on a scalar-cache miss, profiles/r03t.)
 constexpr int RQ_KG = 16;   // vectors per pass
-constexpr int RQ_CPT = 4;   // columns per lane
-constexpr int RQ_RB = 8;    // rows per block (16: sv + acc spilled)
+constexpr int RQ_CPT = 2;   // columns per lane
+constexpr int RQ_RB = 8;    // rows per block (16: the register budget serialised the loads)
 constexpr int RQ_CB = 4 * 64 * RQ_CPT;  // columns per block
 
 __global__ __launch_bounds__(256) void rq_vd_kernel(const float* __restrict__ V, int64_t ldv,
@@ -741,15 +741,18 @@ __global__ __launch_bounds__(256) void rq_part_kernel(const T* __restrict__ S, i
                                                       const double* __restrict__ Vd,
                                                       const float* __restrict__ V, int64_t ldv,
                                                       int k, int ng, double* __restrict__ part) {
-  constexpr int KG = RQ_KG, LG = 4;
+  constexpr int KG = RQ_KG;
   const int kpad = KG * ng;
   __shared__ __attribute__((aligned(16))) double vs[RQ_RB][KG];
   __shared__ double red[4][KG];
+  __shared__ double tw[4][KG][65];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t r0 = (int64_t)blockIdx.y * RQ_RB;
-  const int64_t cw = (int64_t)blockIdx.x * RQ_CB + 256 * wave + lane;
-  // unpredicated loads at clamped in-range addresses (a branch per load otherwise),
-  // out-of-range values zeroed by a select
+  const int64_t cw = (int64_t)blockIdx.x * RQ_CB + 64 * RQ_CPT * wave + lane;
+  // unpredicated, unselected loads at clamped in-range addresses: rows past d meet
+  // zero Vd rows in LDS and columns past d zero epilogue factors, so no condition
+  // touches a loaded value (a uniform row test became a branch per load with a
+  // vmcnt(0) behind each: 32 serialised load latencies per block, 106 us at c1)
   T sv[RQ_RB][RQ_CPT];
 #pragma unroll
   for (int r = 0; r < RQ_RB; ++r)
@@ -757,15 +760,31 @@ __global__ __launch_bounds__(256) void rq_part_kernel(const T* __restrict__ S, i
     for (int u = 0; u < RQ_CPT; ++u) {
       const int64_t c = cw + 64 * u;
       const int64_t rr = r0 + r < d ? r0 + r : d - 1;
-      const T x = S[rr * lds + (c < d ? c : d - 1)];
-      sv[r][u] = (r0 + r < d && c < d) ? x : T(0);
+      sv[r][u] = S[rr * lds + (c < d ? c : d - 1)];
     }
   for (int g = 0; g < ng; ++g) {
   const int j0 = KG * g;
   if (g) __syncthreads();  // the last group's vs / red reads are done
-  for (int e = tid; e < RQ_RB * KG; e += 256) {
-    const int rr = e / KG;
-    vs[rr][e - rr * KG] = r0 + rr < d ? Vd[(r0 + rr) * kpad + j0 + (e - rr * KG)] : 0.0;
+  // (no condition selects a loaded value anywhere below: the compiler turns such a
+  // select into a branch around the load with a vmcnt(0) behind it - masks multiply)
+  if (tid < RQ_RB * KG) {
+    const int rr = tid / KG;
+    const int64_t row = r0 + rr < d ? r0 + rr : d - 1;
+    vs[rr][tid - rr * KG] = Vd[row * kpad + j0 + (tid - rr * KG)] * (r0 + rr < d ? 1.0 : 0.0);
+  }
+  // this group's epilogue factors v_j[c_u], loaded before the FMAs (latency hidden)
+  // (raw values: the column / vector masks are applied in the epilogue, so nothing
+  // consumes a load before the FMAs)
+  float vpre[RQ_CPT][KG];
+#pragma unroll
+  for (int u = 0; u < RQ_CPT; ++u) {
+    const int64_t c = cw + 64 * u;
+    const float* vc = V + (c < d ? c : d - 1);
+#pragma unroll
+    for (int jj = 0; jj < KG; ++jj) {
+      const int j = j0 + jj;
+      vpre[u][jj] = vc[(int64_t)(j < k ? j : k - 1) * ldv];
+    }
   }
   __syncthreads();
   double acc[RQ_CPT][KG];
@@ -789,39 +808,32 @@ __global__ __launch_bounds__(256) void rq_part_kernel(const T* __restrict__ S, i
       for (int jj = 0; jj < KG; ++jj) acc[u][jj] = fma(sd, vv[jj], acc[u][jj]);
     }
   }
-  // (the epilogue's 64 V loads stay below the FMAs: hoisted, they spilled)
-  __builtin_amdgcn_sched_barrier(0);
   double t[KG];
 #pragma unroll
   for (int jj = 0; jj < KG; ++jj) t[jj] = 0.0;
 #pragma unroll
   for (int u = 0; u < RQ_CPT; ++u) {
-    const int64_t c = cw + 64 * u;
-    const float* vc = V + (c < d ? c : d - 1);
+    const double cm = cw + 64 * u < d ? 1.0 : 0.0;
 #pragma unroll
-    for (int jj = 0; jj < KG; ++jj) {
-      const int j = j0 + jj;
-      const float x = vc[(int64_t)(j < k ? j : k - 1) * ldv];
-      t[jj] = fma(acc[u][jj], (c < d && j < k) ? (double)x : 0.0, t[jj]);
-    }
+    for (int jj = 0; jj < KG; ++jj)
+      t[jj] = fma(acc[u][jj], (double)vpre[u][jj] * (j0 + jj < k ? cm : 0.0), t[jj]);
   }
-  // recursive halving over the wave: at step s (mask 32 >> s) a lane keeps the upper
-  // half of its values if its mask bit is set, and adds its partner's copy of them
+  // wave sums of the 16 t_jj through this wave's LDS transpose: lane l (vector
+  // l >> 2, quarter q = l & 3) adds lanes q, q + 4, ... of it, then 2 shuffles.
+  // (Register butterflies with per-lane selects compiled to ~1600 VALU ops per
+  // group - 6x the group's FMAs, profiles/r03x.)  The wave reads only what it wrote:
+  // its LDS operations complete in order, the wave barrier keeps the compiler's.
 #pragma unroll
-  for (int st = 0; st < LG; ++st) {
-    const int m = 32 >> st, h = KG >> (st + 1);
-    const bool up = (lane & m) != 0;
+  for (int jj = 0; jj < KG; ++jj) tw[wave][jj][lane] = t[jj];
+  __builtin_amdgcn_wave_barrier();
+  const int jr = lane >> 2, q = lane & 3;
+  double sum = 0.0;
 #pragma unroll
-    for (int i = 0; i < h; ++i) {
-      const double send = up ? t[i] : t[i + h];
-      const double keep = up ? t[i + h] : t[i];
-      t[i] = keep + __shfl_xor(send, m, 64);
-    }
-  }
-  // lane holds the wave sum of vector lane >> 2 over its group of 4 lanes; fold the
-  // group (commutative adds: every lane of it ends equal)
-  t[0] += __shfl_xor(t[0], 2, 64);
-  t[0] += __shfl_xor(t[0], 1, 64);
+  for (int i = 0; i < 16; ++i) sum += tw[wave][jr][q + 4 * i];
+  sum += __shfl_xor(sum, 1, 64);
+  sum += __shfl_xor(sum, 2, 64);
+  t[0] = sum;
+  __builtin_amdgcn_wave_barrier();  // (the next group's writes stay behind these reads)
   if ((lane & 3) == 0) red[wave][lane >> 2] = t[0];
   __syncthreads();
   if (tid < KG)

@@ -198,9 +198,10 @@ __global__ __launch_bounds__(SYRK_THR) void u8_syrk_kernel(U8Sched s) {
     for (int h = 0; h < 2; ++h) {
       const int c = tid + h * SYRK_THR;
       const int g = c >> 7, fl = c & 127;
+      // (unconditional: a diagonal tile loads its panel twice - a branch around the B
+      // loads would make the compiler's counted waits conservative)
       ra[h] = *reinterpret_cast<const u32x4*>(s.img + img_off(plane, kb, g, i0 + fl, s.nkb, s.fpad));
-      if (!diag)
-        rb[h] = *reinterpret_cast<const u32x4*>(s.img + img_off(plane, kb, g, j0 + fl, s.nkb, s.fpad));
+      rb[h] = *reinterpret_cast<const u32x4*>(s.img + img_off(plane, kb, g, j0 + fl, s.nkb, s.fpad));
     }
   };
   auto put = [&](int st, const u32x4 (&ra)[2], const u32x4 (&rb)[2]) {
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(SYRK_THR) void u8_syrk_kernel(U8Sched s) {
     for (int h = 0; h < 2; ++h) {
       const int c = tid + h * SYRK_THR;
       *reinterpret_cast<u32x4*>(&lds[st][0][c * 16]) = ra[h];
-      if (!diag) *reinterpret_cast<u32x4*>(&lds[st][1][c * 16]) = rb[h];
+      *reinterpret_cast<u32x4*>(&lds[st][1][c * 16]) = rb[h];
     }
   };
 
@@ -265,19 +266,28 @@ __global__ __launch_bounds__(SYRK_THR) void u8_syrk_kernel(U8Sched s) {
   if (!active) return;
   // C/D map (gfx950, dtype independent): column = lane & 15, row = 4 (lane >> 4) + reg
   if constexpr (DIRECT) {
-    long long cjv[4];
+    // every column sum loaded up front at clamped indices (a load inside the i < d
+    // branch waited out its latency alone: 16 serialised loads per wave)
+    long long cjv[4], civ[4][4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int64_t j = j0 + 64 * wj + 16 * b + (lane & 15);
-      cjv[b] = j < s.d ? (long long)s.colsum[j] : 0ll;
+      cjv[b] = (long long)s.colsum[j < s.d ? j : s.d - 1];
     }
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t i = i0 + 64 * wi + 16 * a + 4 * (lane >> 4) + r;
+        civ[a][r] = (long long)s.colsum[i < s.d ? i : s.d - 1];
+      }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t i = i0 + 64 * wi + 16 * a + 4 * (lane >> 4) + r;
         if (i >= s.d) continue;
-        const long long ci = (long long)s.colsum[i];
+        const long long ci = civ[a][r];
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           const int64_t j = j0 + 64 * wj + 16 * b + (lane & 15);
