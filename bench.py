@@ -617,14 +617,16 @@ def run_oneshot(args, cfg, world, rank, dev):
                                     5, stream)
 
     # --- outside the timed region: accuracy, alternative kernel, sweep roofline
-    if concurrent:
+    if concurrent or batched:
         del Ss[1:-1]  # keep worker 0's (S, reused below) and the last worker's buffer
         torch.cuda.empty_cache()
     Xw = X[(W - 1) * ni:W * ni]
     cols = torch.randperm(d, generator=torch.Generator().manual_seed(7))[:16].to(dev)
     Xs = features(Xw).index_select(1, cols)
     S64 = (Xs.t() @ Xs) / ni
-    S_last = Ss[-1] if concurrent else S  # the last worker's covariance
+    # the last worker's covariance (Ss[0] is S = worker 0's in the concurrent and
+    # batched modes; r03y and before compared it with the last worker's rows there)
+    S_last = Ss[-1] if (concurrent or batched) else S
     Sblk = S_last.index_select(0, cols).index_select(1, cols).double()
     sigma_err = float((Sblk - S64).abs().max() / S64.abs().max())
     del Xs
