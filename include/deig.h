@@ -4,8 +4,11 @@
  *
  * Every entry point takes raw device pointers, sizes and leading dimensions (in
  * elements), caller-provided device workspace and a hipStream_t (passed as
- * void*).  The library never allocates or frees device memory and keeps no
- * global mutable state except a thread-local error string.  Work is enqueued on
+ * void*).  The library never allocates or frees device memory.  Its only
+ * process-global state is thread-safe: a thread-local error string, a per-device
+ * CU-count cache (atomics) and a mutex-protected free list of small pinned host
+ * blocks (a few hundred bytes each, allocated on first use and kept) that the
+ * eigensolvers read their per-cycle status from.  Work is enqueued on
  * the given stream; entry points that iterate (the eigensolvers) synchronise that
  * stream between sweeps to test convergence, and return when done.
  *
