@@ -717,7 +717,8 @@ __global__ void unshift_kernel(float* __restrict__ evals, int k, double shift) {
 //                   (an LDS transpose per wave, the 4 waves in order) into
 //                   part[block][16 g + jj];
 //   rq_finish_kernel: block j sums the parts in block order and v_j^T v_j.
-// One read of S, d^2 x kpad fp64 FMA.  (Earlier versions: 32 rows x all
+// One read of the lower block triangle of S, ~d^2 / 2 x kpad fp64 FMA (symmetry: the
+// blocks left of a row block's diagonal panel count twice).  (Earlier versions: 32 rows x all
 // columns per block staged through LDS, 387 us at d = 3072, k = 10 - 3.1 ms of c1's
 // 11.1 ms step, profiles/r03s; one column per lane with the Vd row as scalar loads,
 // 166 us: every row waited on a scalar-cache miss, profiles/r03t.)
@@ -748,6 +749,16 @@ __global__ __launch_bounds__(256) void rq_part_kernel(const T* __restrict__ S, i
   __shared__ double tw[4][KG][65];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t r0 = (int64_t)blockIdx.y * RQ_RB;
+  // S symmetric: only blocks on or below the diagonal panel run (RQ_RB | RQ_CB, so a
+  // row block lies in one column panel); those left of it count twice (exact x2),
+  // the diagonal panel's once.  Skipped blocks write zero parts.
+  const int panel = (int)(r0 / RQ_CB);
+  if ((int)blockIdx.x > panel) {
+    for (int j = tid; j < KG * ng; j += 256)
+      part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (KG * ng) + j] = 0.0;
+    return;
+  }
+  const double wgt = (int)blockIdx.x < panel ? 2.0 : 1.0;
   const int64_t cw = (int64_t)blockIdx.x * RQ_CB + 64 * RQ_CPT * wave + lane;
   // unpredicated, unselected loads at clamped in-range addresses: rows past d meet
   // zero Vd rows in LDS and columns past d zero epilogue factors, so no condition
@@ -838,7 +849,7 @@ __global__ __launch_bounds__(256) void rq_part_kernel(const T* __restrict__ S, i
   __syncthreads();
   if (tid < KG)
     part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kpad + j0 + tid] =
-        ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+        wgt * (((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid]);
   }  // groups
 }
 
