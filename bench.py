@@ -98,6 +98,28 @@ def blas_cores():
         return os.cpu_count()
 
 
+def host_info() -> dict:
+    """The host the CPU baseline ran on (nproc, CPU model,
+    BLAS vendor and version): ``cores`` on a cpu_baseline is the BLAS thread count
+    actually used, which is below nproc where OMP_NUM_THREADS caps it (16 on the GPU box)."""
+    blas = []
+    try:
+        import scipy.linalg  # noqa: F401  (scipy's own OpenBLAS, used by the oracle's eigh)
+        from threadpoolctl import threadpool_info
+        blas = [{"vendor": i.get("internal_api"), "version": i.get("version"),
+                 "library": i.get("prefix"), "threads": i.get("num_threads"),
+                 "architecture": i.get("architecture")}
+                for i in threadpool_info() if i.get("user_api") == "blas"]
+    except Exception:  # pragma: no cover
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):  # pragma: no cover
+        affinity = None
+    return {"nproc": os.cpu_count(), "cpus_in_affinity_mask": affinity,
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"), "blas": blas}
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -191,7 +213,7 @@ def cpu_baseline_oneshot(xs: np.ndarray, n_worker: int, workers: int, k: int,
     best = threaded if threaded is not None and threaded["value"] > v1 else single
     return {
         "value": best["value"], "unit": "samples/s", "cores": cores, "kind": "port",
-        "cpu_model": cpu_model(),
+        "cpu_model": cpu_model(), "host": host_info(),
         "sample": (f"float64 NumPy/SciPy oracle (distributed.py:59-70 + :22-29) on a bounded "
                    f"sample; best of: [{single['note']}]"
                    + (f" and [{threaded['note']}]" if threaded else "")
@@ -209,7 +231,7 @@ def cpu_baseline_oja(pool, V0: torch.Tensor, eta: float, nb: int):
     t = time.perf_counter() - t0
     return {
         "value": nb * b / t, "unit": "samples/s", "cores": int(blas_cores()), "kind": "port",
-        "cpu_model": cpu_model(),
+        "cpu_model": cpu_model(), "host": host_info(),
         "sample": (f"float64 NumPy oracle oja_epoch on {nb} batches of {b} x {xs.shape[1]} "
                    f"(k={V0.shape[1]}): {t:.2f}s; aggregation not counted"),
     }
@@ -247,6 +269,10 @@ def full_time_to_eigenspace(de, synthetic, X, U, n_total: int, k: int, stream) -
     n, d = X.shape
     blocks = n_total // n
     S = torch.zeros((d, d), dtype=torch.float32, device=X.device)
+    # accuracy of the streamed Sigma: a float64 X^T X of 16 sampled features over all
+    # 2^24 rows, accumulated block by block outside the timed launches
+    cols = torch.randperm(d, generator=torch.Generator().manual_seed(7))[:16].to(X.device)
+    S64 = torch.zeros((16, 16), dtype=torch.float64, device=X.device)
     syrk_ms = []
     for b in range(blocks):
         if b > 0:
@@ -254,7 +280,13 @@ def full_time_to_eigenspace(de, synthetic, X, U, n_total: int, k: int, stream) -
         torch.cuda.synchronize()
         syrk_ms.append(time_events(lambda: de.sigma_hat(X, alpha=1.0 / n_total, out=S,
                                                         accumulate=True), 1, stream))
+        Xc = X.index_select(1, cols).double()
+        S64 += Xc.t() @ Xc
+        del Xc
     torch.cuda.synchronize()
+    S64 /= n_total
+    Sblk = S.index_select(0, cols).index_select(1, cols).double()
+    sigma_err = float((Sblk - S64).abs().max() / S64.abs().max())
     t0 = time.perf_counter()
     r = de.topk_eigh(S, k, check_finite=False)
     torch.cuda.synchronize()
@@ -264,8 +296,11 @@ def full_time_to_eigenspace(de, synthetic, X, U, n_total: int, k: int, stream) -
             "covariance_s": cov_s, "solve_s": solve_s, "time_to_eigenspace_s": cov_s + solve_s,
             "samples_per_s": n_total / (cov_s + solve_s), "sweeps": r.sweeps, "resid": r.resid,
             "sin_theta_vs_planted": sin_theta(U, r.V),
-            "note": "one GPU streams all 2^24 rows (config 3's total) through one covariance; "
-                    "block regeneration between launches is untimed (data arrival)"}
+            "sigma_hat_rel_err_vs_f64_sampled": sigma_err,
+            "note": "one GPU streams all 2^24 rows (config 3's total) through one covariance "
+                    "(DEIG_SYRK_ACCUMULATE, tests/test_gpu_syrk_chunks.py); block regeneration "
+                    "between launches is untimed (data arrival); sigma_hat_rel_err_vs_f64_sampled: "
+                    "16 sampled features, float64 over all rows"}
 
 
 def sweep_roofline(de, S: torch.Tensor, p: int, stream) -> dict:
@@ -411,12 +446,30 @@ def timed_loop(step, args, world, dev):
     return elapsed, out
 
 
+def formed_group(args) -> dict:
+    """What the job actually ran on: the process group torch.distributed formed (world
+    size, backend: "nccl" is RCCL on ROCm), the devices this rank sees, and the
+    launcher's WORLD_SIZE - recorded on every line so an N > 1 number can be checked
+    against the ranks that really took part."""
+    formed = dist.is_available() and dist.is_initialized()
+    return {"world_size": dist.get_world_size() if formed else 1,
+            "backend": dist.get_backend() if formed else None,
+            "requested_backend": args.dist_backend if formed else None,
+            "WORLD_SIZE_env": os.environ.get("WORLD_SIZE"),
+            "device_count": torch.cuda.device_count(),
+            "gpus_arg": args.gpus,
+            "note": ("gloo rehearsal: ranks share GPUs, bases staged through host memory - "
+                     "control flow only, not a scaling number")
+            if formed and dist.get_backend() != "nccl" else None}
+
+
 def base_line(args, world, elapsed, total, dtype, config):
     return {
         "metric": METRIC,
         "value": total / elapsed,
         "unit": "samples/s",
         "n_gpus": world,
+        "process_group": formed_group(args),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
@@ -761,25 +814,27 @@ def run_oja(args, cfg, world, rank, dev):
     est = StreamingOja(V0, eta=eta, agg_every=agg)
     stream = torch.cuda.current_stream(dev)
     ev = []
-    agg_t = []
 
     def step(record: bool):
         # one C call for the 64 batches, then the aggregation (gather + solve + broadcast)
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         e[0].record(stream)
         est.block_fn(pool, est.V, est.eta, b, cfg["orth_every"])
         e[1].record(stream)
         est.batches_seen += agg
-        t0 = time.perf_counter()
         est.aggregate()
+        e[2].record(stream)
         torch.cuda.synchronize(dev)
         if record:
             ev.append(e)
-            agg_t.append(time.perf_counter() - t0)
         return None
 
     elapsed, _ = timed_loop(step, args, world, dev)
-    oja_ms = float(np.mean([a.elapsed_time(c) for a, c in ev])) / agg  # per batch
+    oja_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev])) / agg  # per batch
+    # the aggregation (gather + server solve + broadcast) on the device timeline, from
+    # the last Oja batch's end (r03's host clock started when the 64 batches were
+    # enqueued, so it also counted their GPU time)
+    agg_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
     byt = 8.0 * b * d  # Xb read twice (Xb V, then Xb^T T)
     achieved = byt / (oja_ms * 1e-3)
     if rank != 0:
@@ -802,7 +857,8 @@ def run_oja(args, cfg, world, rank, dev):
                         "launch_ms": oja_ms}
     line["cpu_baseline"] = cpu
     line["breakdown"] = {"oja_ms_per_batch": oja_ms,
-                         "aggregate_ms": 1e3 * float(np.mean(agg_t))}
+                         "aggregate_ms": agg_ms,
+                         "aggregate_timing": "HIP events: end of the 64th Oja batch -> end of the aggregation (all-gather + server solve + broadcast), on the launch stream"}
     line["accuracy"] = {"sin_theta_vs_planted": sin_theta(U, est.V),
                         "batches_seen_per_gpu": est.batches_seen}
     return line

@@ -620,6 +620,120 @@ void block_shape(int64_t d, int k, int p_in, int* p_blk, int* kb) {
   }
 }
 
+// Any d (?syevr's contract, distributed.py:29): an explicit S whose dimension the
+// kernels cannot take as it is - d % 4 != 0, d < 16, or a subspace wider than d (k
+// close to a small d) - is staged in the workspace as a zero-padded dp x dp copy, and
+// the solver runs on that.  Its padding directions must never outrank S's own
+// eigenpairs, which a zero padding (eigenvalue 0) would for an indefinite S whose
+// top k reach below 0:
+//  * basis narrower than d: every start basis has zero rows >= d (rr_init's `valid`),
+//    and S Q, the shift, the deflation and Rayleigh-Ritz all keep zero rows zero, so
+//    the padding never enters the iteration;
+//  * basis as wide as the padded space (pb > d, tiny d): the padding diagonal is set
+//    to -(2R) - tiny, R = max_i sum_j |S_ij| >= the spectral radius, strictly below
+//    S's spectrum (the solver then sees an indefinite operator and shifts it).
+// V is computed in the padded space and its first d rows copied out.
+struct Dims {
+  int64_t dp;   // the solver's dimension
+  int pb, kb;   // widest block subspace, pairs per block
+  bool staged;  // S copied into a padded dp x dp image in the workspace
+  bool fill;    // the padding diagonal set below S's spectrum
+};
+
+Dims solver_dims(int64_t d, int k, int p, bool implicit) {
+  Dims m{};
+  m.dp = d;
+  if (!implicit) {
+    int64_t dp = std::max<int64_t>(16, cdiv(d, 4) * 4);
+    int pb, kb;
+    block_shape(dp, k, p, &pb, &kb);
+    if (pb > dp) dp = pb;
+    m.dp = dp;
+  }
+  block_shape(m.dp, k, p, &m.pb, &m.kb);
+  m.staged = m.dp != d;
+  m.fill = m.staged && m.pb > d;
+  return m;
+}
+
+struct Stage {
+  void* S = nullptr;  // dp x dp, element type of the input
+  float* V = nullptr; // dp x k column-major
+  float* Q0 = nullptr;  // dp x pb column-major (warm start)
+};
+
+Stage carve_stage(Carve& c, const Dims& m, int k, int stype) {
+  Stage g;
+  if (!m.staged) return g;
+  const size_t es = stype == DEIG_F64 ? sizeof(double) : sizeof(float);
+  g.S = c.take<char>((size_t)(m.dp * m.dp) * es);
+  g.V = c.take<float>((size_t)m.dp * k);
+  g.Q0 = c.take<float>((size_t)m.dp * m.pb);
+  c.off = align_up(c.off, 256);
+  return g;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void stage_pad_kernel(const T* __restrict__ S, int64_t lds, int64_t d,
+                                                        T* __restrict__ Sp, int64_t dp) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= dp * dp) return;
+  const int64_t i = idx / dp, j = idx - i * dp;
+  Sp[idx] = (i < d && j < d) ? S[i * lds + j] : T(0);
+}
+
+// One workgroup (only for d < pb <= kMaxP): R = max_i sum_j |S_ij| in double, then the
+// padding diagonal entries dp > i >= d set to -(2R) - 1e-30.
+template <typename T>
+__global__ __launch_bounds__(256) void stage_fill_kernel(T* __restrict__ Sp, int64_t dp, int64_t d) {
+  __shared__ double red[256];
+  const int t = threadIdx.x;
+  double m = 0.0;
+  for (int64_t i = t; i < d; i += 256) {
+    double s = 0.0;
+    for (int64_t j = 0; j < d; ++j) s += fabs((double)Sp[i * dp + j]);
+    m = fmax(m, s);
+  }
+  red[t] = m;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (t < w) red[t] = fmax(red[t], red[t + w]);
+    __syncthreads();
+  }
+  const double v = -(2.0 * red[0]) - 1e-30;
+  for (int64_t i = d + t; i < dp; i += 256) Sp[i * dp + i] = (T)v;
+}
+
+// dst[r + j ldd] = r < rows_src ? src[r + j lds] : 0 for r < rows_dst, j < ncol.
+__global__ __launch_bounds__(256) void copy_cols_kernel(const float* __restrict__ src, int64_t lds,
+                                                        int64_t rows_src, float* __restrict__ dst,
+                                                        int64_t ldd, int64_t rows_dst, int ncol) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= rows_dst * ncol) return;
+  const int64_t j = idx / rows_dst, r = idx - j * rows_dst;
+  dst[r + j * ldd] = r < rows_src ? src[r + j * lds] : 0.f;
+}
+
+int copy_cols(const float* src, int64_t lds, int64_t rows_src, float* dst, int64_t ldd,
+              int64_t rows_dst, int ncol, hipStream_t st) {
+  hipLaunchKernelGGL(copy_cols_kernel, dim3((unsigned)cdiv(rows_dst * ncol, 256)), dim3(256), 0, st,
+                     src, lds, rows_src, dst, ldd, rows_dst, ncol);
+  DEIG_HIP_CHECK(hipGetLastError());
+  return DEIG_OK;
+}
+
+template <typename T>
+int stage_matrix(const void* S, int64_t lds, int64_t d, void* Sp, const Dims& m, hipStream_t st) {
+  hipLaunchKernelGGL(stage_pad_kernel<T>, dim3((unsigned)cdiv(m.dp * m.dp, 256)), dim3(256), 0, st,
+                     static_cast<const T*>(S), lds, d, static_cast<T*>(Sp), m.dp);
+  DEIG_HIP_CHECK(hipGetLastError());
+  if (m.fill) {
+    hipLaunchKernelGGL(stage_fill_kernel<T>, dim3(1), dim3(256), 0, st, static_cast<T*>(Sp), m.dp, d);
+    DEIG_HIP_CHECK(hipGetLastError());
+  }
+  return DEIG_OK;
+}
+
 // Top-k eigenpairs (ascending) of the operator.  Blocks of at most kb pairs are
 // solved top-down; each block's converged pairs are LOCKED at the end of V and
 // deflated out of the operator for the blocks below (k > 128 = kMaxP: the Ritz
@@ -644,6 +758,13 @@ struct SolveSM {
   float* V = nullptr;
   int64_t ldv = 0;
   float* evals = nullptr;
+  // staging (solver_dims): the caller's dimension / V, and the rows >= valid of every
+  // start basis that are zero (-1: none)
+  int64_t d_user = 0;
+  float* V_user = nullptr;
+  int64_t ldv_user = 0;
+  bool staged = false;
+  int64_t valid = -1;
   Solver sv;
   bool can_deflate = false;
   double shift = 0.0;
@@ -665,15 +786,47 @@ struct SolveSM {
   SolveSM& operator=(const SolveSM&) = delete;
   ~SolveSM() { status_pool().release(sv.hs); }
 
-  int init(const Operator& op, int64_t d_, int k_, int p, int max_sweeps, float tol, const float* Q0_,
+  int init(const Operator& op_in, int64_t d_, int k_, int p, int max_sweeps, float tol, const float* Q0_,
            int k0_, int64_t ldq0_, float* V_, int64_t ldv_, float* evals_, const Opts& o, void* ws,
            size_t ws_bytes, hipStream_t st) {
-    d = d_;
+    Operator op = op_in;
+    d_user = d_;
     k = k_;
-    DEIG_REQUIRE(d >= 16 && d % 4 == 0, "solver: d=%lld must be >= 16 and a multiple of 4",
-                 (long long)d);
-    DEIG_REQUIRE(k >= 1 && k <= d, "solver: need 1 <= k <= d (k=%d, d=%lld)", k, (long long)d);
-    block_shape(d, k, p, &pb0, &kb);
+    DEIG_REQUIRE(d_ >= 1, "solver: d=%lld must be >= 1", (long long)d_);
+    DEIG_REQUIRE(k >= 1 && k <= d_, "solver: need 1 <= k <= d (k=%d, d=%lld)", k, (long long)d_);
+    if (op.implicit)
+      DEIG_REQUIRE(d_ >= 16 && d_ % 4 == 0, "solver: d=%lld must be >= 16 and a multiple of 4",
+                   (long long)d_);
+    DEIG_REQUIRE(V_ && evals_ && ldv_ >= d_, "solver: bad V / evals / ldv");
+    DEIG_REQUIRE(k0_ >= 0 && (k0_ == 0 || (Q0_ && ldq0_ >= d_)), "solver: bad warm start");
+    const Dims dm = solver_dims(d_, k, p, op.implicit);
+    d = dm.dp;
+    staged = dm.staged;
+    valid = (dm.staged && !dm.fill) ? d_ : -1;
+    Carve cs(ws, ws_bytes);
+    const Stage stg = carve_stage(cs, dm, k, op.stype);
+    if (ws && cs.off > ws_bytes)
+      return fail(DEIG_EWORKSPACE, "solver: workspace %zu bytes < staging %zu", ws_bytes, cs.off);
+    void* ws_solver = ws ? static_cast<char*>(ws) + cs.off : nullptr;
+    const size_t ws_solver_bytes = ws ? ws_bytes - cs.off : 0;
+    if (staged && ws) {
+      int r = op.stype == DEIG_F64 ? stage_matrix<double>(op.S, op.lds, d_, stg.S, dm, st)
+                                   : stage_matrix<float>(op.S, op.lds, d_, stg.S, dm, st);
+      if (r) return r;
+      op.S = stg.S;
+      op.lds = d;
+      if (k0_ > 0) {
+        if ((r = copy_cols(Q0_, ldq0_, d_, stg.Q0, d, d, std::min(k0_, dm.pb), st))) return r;
+        Q0_ = stg.Q0;
+        ldq0_ = d;
+      }
+      V_user = V_;
+      ldv_user = ldv_;
+      V_ = stg.V;
+      ldv_ = d;
+    }
+    pb0 = dm.pb;
+    kb = dm.kb;
     if (k <= kMaxP)
       DEIG_REQUIRE(pb0 % 16 == 0 && pb0 >= k && pb0 <= kMaxP && pb0 <= d,
                    "solver: subspace p=%d must be a multiple of 16 with k <= p <= min(128, d)", pb0);
@@ -681,8 +834,7 @@ struct SolveSM {
       DEIG_REQUIRE(pb0 % 16 == 0 && pb0 >= 2 * kGuard && pb0 <= kMaxP && pb0 <= d,
                    "solver: k=%d > 128 needs a block subspace p in {32, ..., 128} (p=%d)", k, pb0);
     DEIG_REQUIRE(max_sweeps >= 1, "solver: max_sweeps must be >= 1");
-    DEIG_REQUIRE(V_ && evals_ && ldv_ >= d, "solver: bad V / evals / ldv");
-    DEIG_REQUIRE(k0_ >= 0 && k0_ <= pb0 && (k0_ == 0 || (Q0_ && ldq0_ >= d)), "solver: bad warm start");
+    DEIG_REQUIRE(k0_ <= pb0, "solver: warm start k0=%d wider than the subspace p=%d", k0_, pb0);
     const bool image = !op.implicit && o.sweep_algo != DEIG_SWEEP_FP32;
     DEIG_REQUIRE(image || op.implicit || op.stype == DEIG_F32,
                  "solver: a float64 S needs the bf16x6 sweep (DEIG_SWEEP_AUTO)");
@@ -693,9 +845,9 @@ struct SolveSM {
       sv.lam_h = sv.hs->lam;
       sv.res_h = sv.hs->res;
     }
-    sv.w = carve_solver(ws, ws_bytes, d, kb, k, pb0, op.implicit ? op.mk : 0, image, &total);
-    if (!ws || total > ws_bytes)
-      return fail(DEIG_EWORKSPACE, "solver: workspace %zu bytes < required %zu", ws_bytes, total);
+    sv.w = carve_solver(ws_solver, ws_solver_bytes, d, kb, k, pb0, op.implicit ? op.mk : 0, image, &total);
+    if (!ws || total > ws_solver_bytes)
+      return fail(DEIG_EWORKSPACE, "solver: workspace %zu bytes < required %zu", ws_bytes, total + cs.off);
     op0 = op;
     sv.op = op;
     sv.o = o;
@@ -735,11 +887,11 @@ struct SolveSM {
     if ((r = sv.prepare(pb))) return r;
     if (redo) {  // warm start: the block's columns below the dominant pairs
       r = rr_init_launch(sv.w.rr.Z, d, pb, V + (int64_t)(k - locked - warm) * ldv, warm, ldv,
-                         0x5eed5eefull + locked, sv.st);
+                         0x5eed5eefull + locked, sv.st, valid);
     } else if (locked == 0 && k <= kMaxP) {
-      r = rr_init_launch(sv.w.rr.Z, d, pb, Q0, k0, ldq0, 0x5eed5eedull, sv.st);
+      r = rr_init_launch(sv.w.rr.Z, d, pb, Q0, k0, ldq0, 0x5eed5eedull, sv.st, valid);
     } else {
-      r = rr_init_launch(sv.w.rr.Z, d, pb, nullptr, 0, 0, 0x5eed5eedull + locked, sv.st);
+      r = rr_init_launch(sv.w.rr.Z, d, pb, nullptr, 0, 0, 0x5eed5eedull + locked, sv.st, valid);
     }
     if (r) return r;
     sv.iter_begin(kc, pb, Vb, ldv, evb, can_deflate && sv.o.deflate_early && !redo);
@@ -750,7 +902,17 @@ struct SolveSM {
   // The block's iteration has ended: lock / redo / restart / next block.
   int end_block() {
     int r;
-    if (locked > 0 && (r = deflate_orth_launch(Vb, ldv, d, kc, locked, sv.st))) return r;
+    if (locked > 0) {
+      if ((r = deflate_orth_launch(Vb, ldv, d, kc, locked, sv.st))) return r;
+      // A block whose Ritz values sit in the deflation-residue band (k close to d, or
+      // a rank-deficient operator with k > rank: the locked pairs, deflated to ~0,
+      // compete with S's own ~0 eigenvalues) can hold columns that were mostly locked
+      // directions: their projected remainders are valid near-null vectors, but not
+      // orthogonal to each other - re-orthonormalise the block (rare path).
+      bool band = false;
+      for (int j = 0; j < kc; ++j) band |= fabsf(sv.lam_h[j]) <= kNegRel * scale;
+      if (band && (r = block_mgs_launch(Vb, ldv, d, kc, sv.st))) return r;
+    }
     if (locked == 0 && attempt == 0) scale = fmaxf(fabsf(sv.lam_h[0]), fabsf(sv.lam_h[pb - 1]));
     // Indefinite S: the most negative Ritz value of the block against the block's
     // target (and the operator's scale - deflation residue is ~1e-7 of it).
@@ -796,6 +958,7 @@ struct SolveSM {
       r = rq_launch(op0.S, op0.stype, d, op0.lds, V, ldv, k, evals, sv.w.rq, sv.st);
     else if (shift != 0.0)
       r = unshift_launch(evals, k, shift, sv.st);
+    if (!r && staged) r = copy_cols(V, ldv, d, V_user, ldv_user, d_user, k, sv.st);
     state = DONE;
     return r;
   }
@@ -863,7 +1026,8 @@ int solve(const Operator& op0, int64_t d, int k, int p, int max_sweeps, float to
 // streams contending for the hardware queues.
 int solve_batch(int W, const Operator* ops, int64_t d, int k, int p, int max_sweeps, float tol,
                 float* const* V, int64_t ldv, float* const* evals, int* sweeps_out, float* resid_out,
-                const Opts& o, char* ws, size_t ws_each, const hipStream_t* streams, hipStream_t st) {
+                int* status_out, const Opts& o, char* ws, size_t ws_each, const hipStream_t* streams,
+                hipStream_t st) {
   DEIG_REQUIRE(W >= 1 && W <= 1024, "solve_batch: W=%d out of range", W);
   int dev = 0;
   DEIG_HIP_CHECK(hipGetDevice(&dev));
@@ -987,6 +1151,7 @@ int solve_batch(int W, const Operator* ops, int64_t d, int k, int p, int max_swe
     for (int i = 0; i < W; ++i) {
       if (sweeps_out) sweeps_out[i] = sm[i].sv.it;
       if (resid_out) resid_out[i] = sm[i].sv.last;
+      if (status_out) status_out[i] = sm[i].rc ? sm[i].rc : co.err;
     }
     return co.err;
   }
@@ -994,6 +1159,7 @@ int solve_batch(int W, const Operator* ops, int64_t d, int k, int p, int max_swe
   char msg[1024] = "";
   for (int i = 0; i < W; ++i) {
     const int r = sm[i].outcome(sweeps_out ? sweeps_out + i : nullptr, resid_out ? resid_out + i : nullptr);
+    if (status_out) status_out[i] = r;  // each problem's own outcome, as solve() would return it
     if (r && !first) {
       first = r;
       snprintf(msg, sizeof(msg), "%s", g_err);
@@ -1010,7 +1176,7 @@ using namespace deig;
 
 extern "C" {
 
-int deig_version(void) { return 0x000300; }
+int deig_version(void) { return 0x000400; }
 
 const char* deig_last_error(void) { return g_err; }
 
@@ -1029,6 +1195,24 @@ void deig_solver_opts_init(deig_solver_opts* o) {
   o->fast_until = 1e-3f;
   o->round_until = 1e-4f;
   o->debug = 0;
+}
+
+// An explicit S the solver reads in place needs lds % 4 == 0 and 16-byte alignment;
+// a staged one (solver_dims: d % 4 != 0, d < 16, subspace wider than d) only its
+// element alignment.
+static int check_matrix(const void* S, int stype, int64_t d, int k, int p, int64_t lds,
+                        const char* what) {
+  if (!S || lds < d) return fail(DEIG_EINVAL, "%s: need S with lds >= d", what);
+  if (k < 1 || k > d) return fail(DEIG_EINVAL, "%s: need 1 <= k <= d (k=%d, d=%lld)", what, k, (long long)d);
+  const Dims dm = solver_dims(d, k, p, false);
+  const uintptr_t a = reinterpret_cast<uintptr_t>(S);
+  if (dm.staged) {
+    if (a % (stype == DEIG_F64 ? 8 : 4))
+      return fail(DEIG_EINVAL, "%s: S must be aligned to its element size", what);
+  } else if (lds % 4 != 0 || !aligned16(S)) {
+    return fail(DEIG_EINVAL, "%s: S must be 16-byte aligned with lds %% 4 == 0", what);
+  }
+  return DEIG_OK;
 }
 
 static int check_opts(const deig_solver_opts* o) {
@@ -1099,21 +1283,24 @@ int deig_syrk_u8(const uint8_t* X, int64_t n, int64_t d, int64_t ldx, int mode, 
 
 int deig_default_subspace(int64_t d, int k) { return default_subspace(d, k); }
 
-static size_t topk_ws(int64_t d, int k, int p, bool implicit, int64_t mk, const deig_solver_opts* o) {
+static size_t topk_ws(int64_t d, int k, int p, bool implicit, int64_t mk, const deig_solver_opts* o,
+                      int stype = DEIG_F32) {
   const Opts oo = make_opts(o);
-  int pb, kb;
-  block_shape(d, k, p, &pb, &kb);
+  if (d < 1 || k < 1) return 0;
+  const Dims dm = solver_dims(d, k, p, implicit);
+  int pb = dm.pb, kb = dm.kb;
   if (pb < 16) pb = 16;
   if (kb < 1) kb = 1;
   const bool image = !implicit && oo.sweep_algo != DEIG_SWEEP_FP32;
+  Carve c(nullptr, 0);
+  carve_stage(c, dm, k, stype);
   size_t total = 0;
-  carve_solver(nullptr, 0, d, kb, k, pb, implicit ? mk : 0, image, &total);
-  return total;
+  carve_solver(nullptr, 0, dm.dp, kb, k, pb, implicit ? mk : 0, image, &total);
+  return c.off + total;
 }
 
 size_t deig_topk_workspace_ex(int64_t d, int k, int p, int stype, const deig_solver_opts* opts) {
-  (void)stype;
-  return topk_ws(d, k, p, false, 0, opts);
+  return topk_ws(d, k, p, false, 0, opts, stype);
 }
 
 size_t deig_topk_workspace(int64_t d, int k, int p) { return topk_ws(d, k, p, false, 0, nullptr); }
@@ -1126,8 +1313,7 @@ int deig_topk_sym_ex(const void* S, int stype, int64_t d, int64_t lds, int k, in
   if (int rc = check_opts(opts)) return rc;
   if (stype != DEIG_F32 && stype != DEIG_F64)
     return fail(DEIG_EINVAL, "topk: unknown element type %d", stype);
-  if (!S || lds < d || lds % 4 != 0 || !aligned16(S))
-    return fail(DEIG_EINVAL, "topk: S must be 16-byte aligned with lds >= d, lds %% 4 == 0");
+  if (int rc = check_matrix(S, stype, d, k, p, lds, "topk")) return rc;
   Operator op{};
   op.implicit = false;
   op.S = S;
@@ -1147,24 +1333,23 @@ int deig_topk_sym_f32(const float* S, int64_t d, int64_t lds, int k, int p, int 
 
 size_t deig_topk_batch_workspace(int W, int64_t d, int k, int p, int stype,
                                  const deig_solver_opts* opts) {
-  (void)stype;
   if (W < 1) return 0;
-  return (size_t)W * align_up(topk_ws(d, k, p, false, 0, opts), 256);
+  return (size_t)W * align_up(topk_ws(d, k, p, false, 0, opts, stype), 256);
 }
 
 int deig_topk_sym_batch(int W, const void* const* S, int stype, int64_t d, int64_t lds, int k, int p,
                         int max_sweeps, float tol, float* const* V, int64_t ldv, float* const* evals,
-                        int* sweeps_out, float* resid_out, const deig_solver_opts* opts, void* ws,
-                        size_t ws_bytes, void* const* streams, void* stream) {
+                        int* sweeps_out, float* resid_out, int* status_out,
+                        const deig_solver_opts* opts, void* ws, size_t ws_bytes,
+                        void* const* streams, void* stream) {
   g_err[0] = 0;
   if (int rc = check_opts(opts)) return rc;
   if (W < 1 || !S || !V || !evals) return fail(DEIG_EINVAL, "topk_batch: need W >= 1 and S / V / evals arrays");
   if (stype != DEIG_F32 && stype != DEIG_F64)
     return fail(DEIG_EINVAL, "topk_batch: unknown element type %d", stype);
   for (int i = 0; i < W; ++i)
-    if (!S[i] || lds < d || lds % 4 != 0 || !aligned16(S[i]))
-      return fail(DEIG_EINVAL, "topk_batch: S[%d] must be 16-byte aligned with lds >= d, lds %% 4 == 0", i);
-  const size_t each = align_up(topk_ws(d, k, p, false, 0, opts), 256);
+    if (int rc = check_matrix(S[i], stype, d, k, p, lds, "topk_batch")) return rc;
+  const size_t each = align_up(topk_ws(d, k, p, false, 0, opts, stype), 256);
   if (!ws || ws_bytes < (size_t)W * each)
     return fail(DEIG_EWORKSPACE, "topk_batch: workspace %zu bytes < required %zu", ws_bytes,
                 (size_t)W * each);
@@ -1179,7 +1364,8 @@ int deig_topk_sym_batch(int W, const void* const* S, int stype, int64_t d, int64
     sts[i] = streams && streams[i] ? (hipStream_t)streams[i] : (hipStream_t)stream;
   }
   return solve_batch(W, ops.data(), d, k, p, max_sweeps, tol, V, ldv, evals, sweeps_out, resid_out,
-                     make_opts(opts), static_cast<char*>(ws), each, sts.data(), (hipStream_t)stream);
+                     status_out, make_opts(opts), static_cast<char*>(ws), each, sts.data(),
+                     (hipStream_t)stream);
 }
 
 size_t deig_projavg_workspace_ex(int64_t d, int64_t mk, int k, int p,

@@ -149,8 +149,9 @@ struct RRBuffers {
   float* resid;      // k  (relative residual per top-k column; [k] = max)
   int* info;         // small int scratch
 };
+// Start basis (Q0's k0 columns, then pseudo-random ones); rows >= valid zero (< 0: none).
 int rr_init_launch(float* Z, int64_t d, int p, const float* Q0, int k0, int64_t ldq0,
-                   uint64_t seed, hipStream_t stream);
+                   uint64_t seed, hipStream_t stream, int64_t valid = -1);
 // max_jsweeps caps the Jacobi sweeps of the small eigenproblem (30 = converge);
 // jrel: a pair is rotated while |h_ab| > jrel sqrt(|h_aa h_bb|) (2e-7: to rounding).
 int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream, int max_jsweeps = 30,
@@ -168,6 +169,9 @@ int rr_update_launch(const RRBuffers& b, int64_t d, int p, int k, float* V, int6
                      float* evals, hipStream_t stream);
 // Columns 0..kc-1 of V (col-major, ldv) made orthogonal to columns kc..kc+r-1, normalised.
 int deflate_orth_launch(float* V, int64_t ldv, int64_t d, int kc, int r, hipStream_t stream);
+// Columns 0..kc-1 of V orthonormalised among themselves in order (modified Gram-Schmidt,
+// one launch per column; the rare path of a block in the deflation-residue band).
+int block_mgs_launch(float* V, int64_t ldv, int64_t d, int kc, hipStream_t stream);
 // evals[0..k) -= shift (device).
 int unshift_launch(float* evals, int k, double shift, hipStream_t stream);
 // evals[j] = v_j^T S v_j / v_j^T v_j in double for the k columns of V (S: stype).

@@ -37,15 +37,20 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
+// Start basis: Q0's k0 columns, then pseudo-random columns.  Rows >= valid are zero
+// (the zero padding of a staged S, capi.hip: its directions then never enter the
+// basis - S Q, the shift, deflation and Rayleigh-Ritz all keep zero rows zero).
 __global__ __launch_bounds__(256) void rr_init_kernel(float* __restrict__ Z, int64_t d, int p,
                                                       const float* __restrict__ Q0, int k0,
-                                                      int64_t ldq0, uint64_t seed) {
+                                                      int64_t ldq0, uint64_t seed, int64_t valid) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= d * p) return;
   const int64_t r = idx / p;
   const int j = (int)(idx - r * p);
   float v;
-  if (j < k0) {
+  if (r >= valid) {
+    v = 0.f;
+  } else if (j < k0) {
     v = Q0[r + (int64_t)j * ldq0];
   } else {
     const uint64_t h = mix64(seed ^ mix64((uint64_t)r * 0x100000001B3ull + (uint64_t)j));
@@ -647,14 +652,17 @@ __global__ __launch_bounds__(256) void cheb_step_kernel(float* __restrict__ Z,
 // right, and projecting v^ out is exact to O(lam_1 |d|^2).  One block per column;
 // V_D in chunks of 8 columns (modified Gram-Schmidt by chunk, twice when r > 8:
 // block locking of k > 128 pairs); fixed-order block reductions.
-__global__ __launch_bounds__(256) void deflate_orth_kernel(float* __restrict__ V, int64_t ldv,
-                                                           int64_t d, int kc, int r) {
+// (block_mgs: the same kernel with Vd = the block's own earlier columns, one column
+// per launch - see deflate_orth_launch.)
+__global__ __launch_bounds__(256) void deflate_orth_kernel(float* __restrict__ V,
+                                                           const float* __restrict__ Vd,
+                                                           int64_t ldv, int64_t d, int r,
+                                                           int passes) {
   __shared__ float red[4][8];
   __shared__ float coef[8];
   const int j = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   float* v = V + (int64_t)j * ldv;
-  const float* vd0 = V + (int64_t)kc * ldv;
-  const int passes = r > 8 ? 2 : 1;
+  const float* vd0 = Vd;
   for (int pass = 0; pass < passes; ++pass)
     for (int q0 = 0; q0 < r; q0 += 8) {
       const int nq = r - q0 < 8 ? r - q0 : 8;
@@ -888,10 +896,10 @@ size_t rr_small_shm(int p) {
 }  // namespace
 
 int rr_init_launch(float* Z, int64_t d, int p, const float* Q0, int k0, int64_t ldq0,
-                   uint64_t seed, hipStream_t stream) {
+                   uint64_t seed, hipStream_t stream, int64_t valid) {
   const int64_t tot = d * p;
   hipLaunchKernelGGL(rr_init_kernel, dim3((unsigned)cdiv(tot, 256)), dim3(256), 0, stream, Z, d,
-                     p, Q0, k0, ldq0, seed);
+                     p, Q0, k0, ldq0, seed, valid < 0 ? d : valid);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }
@@ -957,8 +965,26 @@ int cheb_step_launch(const RRBuffers& b, float* T, int64_t d, int p, float thr, 
 
 int deflate_orth_launch(float* V, int64_t ldv, int64_t d, int kc, int r, hipStream_t stream) {
   DEIG_REQUIRE(r >= 1 && kc >= 1, "deflate_orth: r=%d kc=%d out of range", r, kc);
-  hipLaunchKernelGGL(deflate_orth_kernel, dim3(kc), dim3(256), 0, stream, V, ldv, d, kc, r);
+  hipLaunchKernelGGL(deflate_orth_kernel, dim3(kc), dim3(256), 0, stream, V, V + (int64_t)kc * ldv,
+                     ldv, d, r, r > 8 ? 2 : 1);
   DEIG_HIP_CHECK(hipGetLastError());
+  return DEIG_OK;
+}
+
+int block_mgs_launch(float* V, int64_t ldv, int64_t d, int kc, hipStream_t stream) {
+  DEIG_REQUIRE(kc >= 1, "block_mgs: kc=%d out of range", kc);
+  // column j against columns 0 .. j-1 (already orthonormal), in order, projected
+  // twice (a column that was mostly locked directions keeps a small remainder) and
+  // normalised
+  for (int j = 0; j < kc; ++j) {
+    if (j == 0) {
+      hipLaunchKernelGGL(deflate_orth_kernel, dim3(1), dim3(256), 0, stream, V, V, ldv, d, 0, 1);
+    } else {
+      hipLaunchKernelGGL(deflate_orth_kernel, dim3(1), dim3(256), 0, stream, V + (int64_t)j * ldv, V,
+                         ldv, d, j, 2);
+    }
+    DEIG_HIP_CHECK(hipGetLastError());
+  }
   return DEIG_OK;
 }
 

@@ -93,21 +93,29 @@ def _device_copy(data) -> torch.Tensor:
         return data
     if not torch.cuda.is_available():
         raise RuntimeError("SlaveNode: needs a ROCm GPU; there is no CPU fallback")
-    arr = data if isinstance(data, np.ndarray) else None
+    if isinstance(data, np.ndarray):
+        # a read-only array that owns its memory cannot change: no sampling pass
+        owned_ro = not data.flags.writeable and data.base is None
+        fp = (data.shape, data.dtype.str, "ro") if owned_ro else _fingerprint(data)
+    elif isinstance(data, torch.Tensor):
+        # a CPU tensor: its storage and in-place version counter say whether it changed
+        fp = (tuple(data.shape), str(data.dtype), data.data_ptr(), data._version)
+    else:
+        fp = None  # other array-likes: converted on every call, never cached
     key = id(data)
-    fp = _fingerprint(arr) if arr is not None else None
-    with _dev_lock:
-        hit = _dev_cache.get(key)
-        if hit is not None and hit[0]() is data and hit[1] == fp:
-            return hit[2]
+    if fp is not None:
+        with _dev_lock:
+            hit = _dev_cache.get(key)
+            if hit is not None and hit[0]() is data and hit[1] == fp:
+                return hit[2]
     t = torch.as_tensor(data)
     if t.dtype == torch.uint8:
         dev = t.to(torch.device("cuda", torch.cuda.current_device()))
     else:
         dev = linalg.require_device_tensor(t, "SlaveNode.data", keep_f64=True)
-    if arr is not None:
+    if fp is not None:
         try:
-            ref = weakref.ref(arr, lambda _r, k=key: _drop(k))
+            ref = weakref.ref(data, lambda _r, k=key: _drop(k))
         except TypeError:  # not weak-referenceable: no caching
             return dev
         with _dev_lock:

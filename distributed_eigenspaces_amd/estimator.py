@@ -19,6 +19,7 @@ per-worker compute is injectable for those tests and defaults to the GPU ops.
 """
 from __future__ import annotations
 
+import inspect
 from dataclasses import dataclass
 
 import torch
@@ -42,23 +43,29 @@ def rank_shards(n_rows: int, world: int, rank: int, workers_per_rank: int = 1):
     return allr[rank * workers_per_rank:(rank + 1) * workers_per_rank]
 
 
+def comm_tensor(t: torch.Tensor, group=None) -> torch.Tensor:
+    """The tensor the process group's backend moves for ``t``: ``t`` itself (RCCL
+    moves device tensors over xGMI; gloo moves host tensors), or a host copy of a
+    device tensor under gloo (the multi-rank rehearsal, several ranks sharing one
+    GPU).  The collective calls are the same on both backends; only this staging
+    differs."""
+    if t.is_cuda and dist.get_backend(group) != "nccl":
+        return t.cpu()
+    return t
+
+
 def gather_bases(Wt_local: torch.Tensor, group=None) -> torch.Tensor:
-    """All-gather the per-rank stacks of bases ((W k) x d each) in rank order."""
+    """All-gather the per-rank stacks of bases ((W k) x d each) in rank order: ONE
+    ``all_gather_into_tensor`` (ncclAllGather under RCCL) into Wt = [V_1^T; ...; V_M^T]."""
     if not dist.is_available() or not dist.is_initialized():
         return Wt_local
     world = dist.get_world_size(group)
     if world == 1:
         return Wt_local
-    src = Wt_local.contiguous()
-    if dist.get_backend(group) == "gloo" and src.is_cuda:
-        # rehearsal path (several ranks sharing one GPU): gloo gathers host tensors
-        host = src.cpu()
-        parts = [torch.empty_like(host) for _ in range(world)]
-        dist.all_gather(parts, host, group=group)
-        return torch.cat(parts, dim=0).to(src.device)
+    src = comm_tensor(Wt_local.contiguous(), group)
     out = torch.empty((world * src.shape[0], src.shape[1]), dtype=src.dtype, device=src.device)
     dist.all_gather_into_tensor(out, src, group=group)
-    return out
+    return out.to(Wt_local.device)
 
 
 @dataclass
@@ -69,6 +76,14 @@ class EstimatorResult:
     worker_evals: list             # this rank's workers' eigenvalues
     sweeps_worker: list
     sweeps_server: int
+
+
+def _batch_accepts(solver_kw: dict) -> bool:
+    """The batched worker solve takes these solver options (topk_eigh_batch has no
+    per-problem warm start q0, for one): others fall back to the serial worker loop,
+    which passes them to topk_eigh as before."""
+    params = inspect.signature(linalg.topk_eigh_batch).parameters
+    return all(key in params and key not in ("Ss", "k") for key in solver_kw)
 
 
 def _gpu_worker(x: torch.Tensor, k: int, **kw):
@@ -107,7 +122,7 @@ class DistributedEigenspaceEstimator:
         parts = shard_ranges(X_local.shape[0], self.wpr)
         if self.concurrent and len(parts) > 1 and X_local.is_cuda:
             return self._local_bases_concurrent(X_local, parts)
-        if self.batched and len(parts) > 1 and X_local.is_cuda:
+        if self.batched and len(parts) > 1 and X_local.is_cuda and _batch_accepts(self.solver_kw):
             Ss = [linalg.sigma_hat(X_local[lo:hi]) for lo, hi in parts]
             rs = linalg.topk_eigh_batch(Ss, self.k, check_finite=False, **self.solver_kw)
             return (torch.cat([r.V.t() for r in rs], dim=0).contiguous(), [r.evals for r in rs],

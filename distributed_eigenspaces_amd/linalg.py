@@ -322,6 +322,19 @@ def _warm(q0, d, device):
     return q, q.shape[1], q.stride(1)
 
 
+def _solver_matrix(S: torch.Tensor) -> torch.Tensor:
+    """S as the solver reads it: unit column stride; when the library reads it in
+    place (d % 4 == 0: include/deig.h deig_topk_sym_ex) also a row stride % 4 == 0 and
+    16-byte alignment.  Other dimensions are staged by the library itself (a zero-padded
+    copy in the workspace whose padding never enters the result), so no padding here."""
+    d = S.shape[0]
+    if S.stride(1) != 1 or S.stride(0) < d:
+        S = S.contiguous()
+    if d % 4 == 0 and (S.stride(0) % 4 or S.data_ptr() % 16):
+        S = S.clone(memory_format=torch.contiguous_format)
+    return S
+
+
 def topk_eigh(S: torch.Tensor, k: int, *, p: int | None = None, tol: float = DEFAULT_TOL,
               max_sweeps: int = DEFAULT_MAX_SWEEPS, q0: torch.Tensor | None = None,
               check_finite: bool = True, opts: "_lib.SolverOpts | None" = None) -> EigResult:
@@ -329,17 +342,16 @@ def topk_eigh(S: torch.Tensor, k: int, *, p: int | None = None, tol: float = DEF
 
     GPU replacement for ``Node.top_k_eigenvectors`` (distributed.py:22-29:
     ``eigh(matrix, eigvals=(N-k, N-1))[1]``) that also returns the eigenvalues.
-    Like scipy's ``?syevr`` call it takes any symmetric S and any 1 <= k <= d
-    (ValueError outside, like scipy's subset_by_index check): k > 128 runs in
-    locked blocks of p - 16 pairs, and an indefinite S is detected from the Ritz
-    values and solved as S + sigma I (include/deig.h deig_topk_sym_ex).  A float64
-    S (the reference's dtype) is read in double by the image and deflation passes.
-    Only the lower triangle matters mathematically, but the full matrix is read
-    (the SYRK output is bit-exactly symmetric).  Zero padding (d % 4 != 0, or a
-    subspace wider than d when k is close to d) adds zero eigenvalues: for a
-    rank-deficient S whose top-k reaches into its null space those k-th vectors
-    are arbitrary null-space vectors, as with eigh, but may lie partly in the
-    padding.  ``opts``: solver options (``_lib.solver_opts(...)``).
+    Like scipy's ``?syevr`` call it takes any symmetric S of any size d and any
+    1 <= k <= d (ValueError outside, like scipy's subset_by_index check): k > 128 runs
+    in locked blocks of p - 16 pairs, an indefinite S is detected from the Ritz values
+    and solved as S + sigma I, and a d the kernels cannot take as is (d % 4 != 0,
+    d < 16, a subspace wider than d) is staged by the library in a padded copy whose
+    padding directions never outrank S's own eigenpairs (include/deig.h
+    deig_topk_sym_ex).  A float64 S (the reference's dtype) is read in double by the
+    image and deflation passes.  Only the lower triangle matters mathematically, but
+    the full matrix is read (the SYRK output is bit-exactly symmetric).  ``opts``:
+    solver options (``_lib.solver_opts(...)``).
     """
     S = require_device_tensor(S, "topk_eigh", keep_f64=True)
     if S.dim() != 2 or S.shape[0] != S.shape[1]:
@@ -350,38 +362,24 @@ def topk_eigh(S: torch.Tensor, k: int, *, p: int | None = None, tol: float = DEF
         raise ValueError(f"k={k} out of range [1, {d}]")
     if check_finite and not bool(torch.isfinite(S).all()):
         raise ValueError("array must not contain infs or NaNs")
-    dp = _pad_dim(d)
-    if not p:  # a subspace wider than d (k close to a small d): pad d up to it
-        dp = max(dp, default_subspace(max(dp, (min(k, MAX_P) + 15) // 16 * 16), k))
-    align = 32 if S.dtype == torch.float64 else 16
-    if dp != d or S.stride(1) != 1 or S.stride(0) % 4 or S.data_ptr() % align:
-        Sp = torch.zeros((dp, dp), dtype=S.dtype, device=S.device)
-        Sp[:d, :d] = S
-        S = Sp
+    S = _solver_matrix(S)
     q, k0, ldq = _warm(q0, d, S.device)
-    if q is not None and dp != d:
-        qp = torch.zeros((dp, k0), dtype=torch.float32, device=S.device)
-        qp[:d] = q
-        q, ldq = qp.t().contiguous().t(), dp
-    pp = int(p) if p else default_subspace(dp, k)
+    pp = int(p) if p else 0
     stype = _lib.DEIG_F64 if S.dtype == torch.float64 else _lib.DEIG_F32
     o = opts if opts is not None else _lib.solver_opts()
-    V = _colmajor(dp, k, S.device)
+    V = _colmajor(d, k, S.device)
     evals = torch.empty(k, dtype=torch.float32, device=S.device)
     sweeps, resid = ctypes.c_int(0), ctypes.c_float(0)
     L = _lib.lib()
     with torch.cuda.device(S.device):
-        nbytes = L.deig_topk_workspace_ex(dp, k, pp, stype, ctypes.byref(o))
+        nbytes = L.deig_topk_workspace_ex(d, k, pp, stype, ctypes.byref(o))
         ws = _workspace(S.device, nbytes)
-        rc = L.deig_topk_sym_ex(S.data_ptr(), stype, dp, S.stride(0), k, pp, int(max_sweeps),
+        rc = L.deig_topk_sym_ex(S.data_ptr(), stype, d, S.stride(0), k, pp, int(max_sweeps),
                                 ctypes.c_float(tol), q.data_ptr() if q is not None else None,
-                                k0, ldq, V.data_ptr(), dp, evals.data_ptr(),
+                                k0, ldq, V.data_ptr(), d, evals.data_ptr(),
                                 ctypes.byref(sweeps), ctypes.byref(resid), ctypes.byref(o),
                                 ws.data_ptr(), nbytes, _stream(S.device))
-    res = _finish(rc, V, evals, sweeps, resid, "deig_topk_sym_ex")
-    if dp != d:
-        res.V = res.V[:d].t().contiguous().t()
-    return res
+    return _finish(rc, V, evals, sweeps, resid, "deig_topk_sym_ex")
 
 
 _batch_streams = threading.local()
@@ -424,31 +422,20 @@ def topk_eigh_batch(Ss, k: int, *, p: int | None = None, tol: float = DEFAULT_TO
     k = int(k)
     if not 1 <= k <= d:
         raise ValueError(f"k={k} out of range [1, {d}]")
-    dp = _pad_dim(d)
-    if not p:
-        dp = max(dp, default_subspace(max(dp, (min(k, MAX_P) + 15) // 16 * 16), k))
-    align = 32 if dt == torch.float64 else 16
-    lds = dp
-    mats = []
-    for S in Ss:
-        if dp != d or S.stride(1) != 1 or S.stride(0) != Ss[0].stride(0) or S.stride(0) % 4 \
-                or S.data_ptr() % align:
-            Sp = torch.zeros((dp, dp), dtype=dt, device=dev)
-            Sp[:d, :d] = S
-            S = Sp
-        mats.append(S)
+    mats = [_solver_matrix(S) for S in Ss]
     lds = mats[0].stride(0)
     if any(S.stride(0) != lds for S in mats):
-        mats = [S if S.stride(0) == dp else S.contiguous() for S in mats]
-        lds = dp
+        mats = [S.contiguous() for S in mats]
+        lds = d
     W = len(mats)
-    pp = int(p) if p else default_subspace(dp, k)
+    pp = int(p) if p else 0
     stype = _lib.DEIG_F64 if dt == torch.float64 else _lib.DEIG_F32
     o = opts if opts is not None else _lib.solver_opts()
-    Vs = [_colmajor(dp, k, dev) for _ in range(W)]
+    Vs = [_colmajor(d, k, dev) for _ in range(W)]
     evs = [torch.empty(k, dtype=torch.float32, device=dev) for _ in range(W)]
     sweeps = (ctypes.c_int * W)()
     resid = (ctypes.c_float * W)()
+    status = (ctypes.c_int * W)()
     vp = ctypes.c_void_p
     S_arr = (vp * W)(*[S.data_ptr() for S in mats])
     V_arr = (vp * W)(*[V.data_ptr() for V in Vs])
@@ -460,24 +447,20 @@ def topk_eigh_batch(Ss, k: int, *, p: int | None = None, tol: float = DEFAULT_TO
     st_arr = (vp * W)(*[s.cuda_stream for s in side])
     L = _lib.lib()
     with torch.cuda.device(dev):
-        nbytes = L.deig_topk_batch_workspace(W, dp, k, pp, stype, ctypes.byref(o))
+        nbytes = L.deig_topk_batch_workspace(W, d, k, pp, stype, ctypes.byref(o))
         ws = _workspace(dev, nbytes)
-        rc = L.deig_topk_sym_batch(W, S_arr, stype, dp, lds, k, pp, int(max_sweeps), ctypes.c_float(tol),
-                                   V_arr, dp, E_arr, sweeps, resid, ctypes.byref(o), ws.data_ptr(),
-                                   nbytes, st_arr, cur.cuda_stream)
+        rc = L.deig_topk_sym_batch(W, S_arr, stype, d, lds, k, pp, int(max_sweeps), ctypes.c_float(tol),
+                                   V_arr, d, E_arr, sweeps, resid, status, ctypes.byref(o),
+                                   ws.data_ptr(), nbytes, st_arr, cur.cuda_stream)
     for t in mats + Vs + evs:  # used on the side streams
         for s in side:
             t.record_stream(s)
     _lib.check(rc, "deig_topk_sym_batch")
-    conv = rc == _lib.DEIG_OK
-    if not conv:
+    if rc != _lib.DEIG_OK:
         warnings.warn(f"deig_topk_sym_batch: {_lib.last_error()}", _lib.NotConvergedWarning, stacklevel=2)
-    out = []
-    for i in range(W):
-        V = Vs[i] if dp == d else Vs[i][:d].t().contiguous().t()
-        out.append(EigResult(evals=evs[i], V=V, sweeps=int(sweeps[i]), resid=float(resid[i]),
-                             converged=conv and float(resid[i]) <= max(float(tol), 0.0) * 4 + 2e-6))
-    return out
+    # each problem's own outcome (status[i]: what deig_topk_sym_ex would have returned)
+    return [EigResult(evals=evs[i], V=Vs[i], sweeps=int(sweeps[i]), resid=float(resid[i]),
+                      converged=int(status[i]) == _lib.DEIG_OK) for i in range(W)]
 
 
 def stack_bases(bases) -> torch.Tensor:

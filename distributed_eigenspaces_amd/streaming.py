@@ -25,7 +25,7 @@ import torch
 import torch.distributed as dist
 
 from . import linalg
-from .estimator import gather_bases
+from .estimator import comm_tensor, gather_bases
 
 __all__ = ["StreamingOja", "broadcast_basis"]
 
@@ -40,12 +40,10 @@ def broadcast_basis(Vt: torch.Tensor, src: int, group=None) -> torch.Tensor:
     """Broadcast a contiguous k x d basis image from ``src`` (in place)."""
     if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
         return Vt
-    if dist.get_backend(group) == "gloo" and Vt.is_cuda:
-        host = Vt.cpu()  # rehearsal path: gloo moves host tensors
-        dist.broadcast(host, src=src, group=group)
-        Vt.copy_(host)
-        return Vt
-    dist.broadcast(Vt, src=src, group=group)
+    buf = comm_tensor(Vt, group)  # Vt itself under RCCL, a host copy under gloo
+    dist.broadcast(buf, src=src, group=group)
+    if buf is not Vt:
+        Vt.copy_(buf)
     return Vt
 
 

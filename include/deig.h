@@ -42,7 +42,7 @@ extern "C" {
 #define DEIG_F32 0
 #define DEIG_F64 1
 
-/* Library version, e.g. 0x000300 for 0.3.0. */
+/* Library version, e.g. 0x000400 for 0.4.0. */
 int deig_version(void);
 
 /* Thread-local message for the last nonzero return on this thread ("" if none). */
@@ -206,7 +206,11 @@ void deig_solver_opts_init(deig_solver_opts* opts);
  * Replaces Node.top_k_eigenvectors  distributed.py:22-29
  * (scipy.linalg.eigh(S, eigvals=(d-k, d-1))[1]  ->  LAPACK dsyevr), plus the
  * eigenvalues ([0] of the same call) as a side output.
- * Any 1 <= k <= d and any symmetric S, like ?syevr.
+ * Any d >= 1, any 1 <= k <= d and any symmetric S, like ?syevr.  S is read in place
+ * when d % 4 == 0, d >= 16 and the subspace fits in d (then lds % 4 == 0 and a 16-byte
+ * aligned S are required); otherwise it is staged as a zero-padded copy in the
+ * workspace (any lds >= d, element alignment) whose padding never enters the
+ * iteration or the result (deig_topk_workspace_ex accounts for it).
  * Block subspace iteration with Rayleigh-Ritz on a p-dimensional subspace
  * (k <= p <= 128, p % 16 == 0, p <= d; k > 128: blocks of p - 16 pairs on a p-column
  * subspace, p = 128 by default, each block's pairs LOCKED and deflated out of S for
@@ -260,15 +264,18 @@ int deig_projavg_topk_f32(const float* Wt, int64_t d, int64_t mk, int64_t ldw,
  * for its sweeps and updates (NULL array or entries: `stream`); the batched small
  * solves run on `stream`, and on return every problem's work has been joined into
  * `stream`.  Workspace: deig_topk_batch_workspace(W, ...) bytes.  Returns the
- * first error; DEIG_NOT_CONVERGED if any problem stopped above tol.
+ * first error; DEIG_NOT_CONVERGED if any problem stopped above tol.  status_out[i]
+ * (host array, may be NULL): problem i's own return code, the one deig_topk_sym_ex
+ * would have returned for it.
  * Replaces W concurrent Node.top_k_eigenvectors calls (distributed.py:22-29, one
  * per SlaveNode shard :42-53). */
 size_t deig_topk_batch_workspace(int W, int64_t d, int k, int p, int stype,
                                  const deig_solver_opts* opts);
 int deig_topk_sym_batch(int W, const void* const* S, int stype, int64_t d, int64_t lds, int k, int p,
                         int max_sweeps, float tol, float* const* V, int64_t ldv, float* const* evals,
-                        int* sweeps_out, float* resid_out, const deig_solver_opts* opts, void* ws,
-                        size_t ws_bytes, void* const* streams, void* stream);
+                        int* sweeps_out, float* resid_out, int* status_out,
+                        const deig_solver_opts* opts, void* ws, size_t ws_bytes,
+                        void* const* streams, void* stream);
 
 size_t deig_projavg_workspace(int64_t d, int64_t mk, int k, int p);
 /* With options (k > 128: block locking with the locked pairs deflated by products

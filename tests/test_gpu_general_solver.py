@@ -119,3 +119,79 @@ def test_projector_average_k_above_128(cuda):
     Pd = ref_cpu.projector_distance(r.V.cpu().numpy(), V)
     assert Pd <= P_TOL, Pd
     np.testing.assert_allclose(r.evals.double().cpu().numpy(), w, rtol=EV_TOL, atol=1e-6)
+
+
+@pytest.mark.parametrize("d,k,case", [(766, 5, "negative_definite"), (766, 12, "mixed"),
+                                      (10, 3, "negative_definite"), (13, 4, "mixed"),
+                                      (20, 18, "negative_definite")])
+def test_indefinite_padded_dimension(d, k, case, cuda):
+    """d % 4 != 0 or d < 16 (the library stages S in a zero-padded copy): the padding's
+    eigenvalue-0 directions must not outrank S's own negative top-k eigenpairs (r03
+    padded in Python and returned them as converged zero columns).  d = 766:
+    the start basis has zero padding rows; d = 10 / 13 / 20: the basis spans the padded
+    space, whose diagonal is set below S's spectrum."""
+    import distributed_eigenspaces_amd as de
+    if case == "negative_definite":
+        lam = -np.linspace(1.0, 40.0, d)
+    else:  # top k straddle zero, most of the spectrum negative
+        lam = np.concatenate([np.linspace(2.0, 1.0, k // 2), -np.linspace(0.5, 1.5, k - k // 2),
+                              -np.linspace(3.0, 30.0, d - k)])
+    S, S_h = planted(d, lam, seed=d + k, device=cuda)
+    r = de.topk_eigh(S.float(), k)
+    assert r.V.shape == (d, k)
+    check(r, S.float().double().cpu().numpy(), k)
+    Vh = r.V.double().cpu().numpy()
+    np.testing.assert_allclose(Vh.T @ Vh, np.eye(k), atol=1e-5)
+    # the float64 S and the batched solver take the same staging
+    r64 = de.topk_eigh(S, k)
+    check(r64, S_h, k)
+    rb = de.topk_eigh_batch([S.float(), S.float()], k)
+    for x in rb:
+        check(x, S.float().double().cpu().numpy(), k)
+
+
+def test_batch_status_is_per_problem(cuda):
+    """One batched solve of an easy and an impossible problem (gap 0.999, 40 sweeps):
+    each result's converged flag is that problem's own outcome (one
+    unconverged problem used to mark every problem unconverged)."""
+    import warnings
+
+    import distributed_eigenspaces_amd as de
+    from distributed_eigenspaces_amd import _lib
+    d, k = 512, 8
+    easy, _ = planted(d, spectrum(d, k), seed=21, device=cuda)
+    hard, _ = planted(d, np.concatenate([np.linspace(2.0, 1.0, k), np.linspace(0.999, 0.5, d - k)]),
+                      seed=22, device=cuda)
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        rs = de.topk_eigh_batch([easy.float(), hard.float()], k, max_sweeps=40)
+    assert any(issubclass(x.category, _lib.NotConvergedWarning) for x in rec)
+    assert rs[0].converged and not rs[1].converged
+    single = de.topk_eigh(easy.float(), k, max_sweeps=40)
+    assert torch.equal(single.V, rs[0].V) and torch.equal(single.evals, rs[0].evals)
+
+
+def test_k_above_128_rank_deficient(cuda):
+    """k = 200 > 128 on a rank-100 PSD covariance (n = 100 rows, d = 512): the second
+    block's pairs are S's null space, where the deflated locked pairs (~0) compete; V
+    must stay orthonormal, the top-100 subspace match eigh, the null
+    pairs' eigenvalues be ~0 and every residual small."""
+    import distributed_eigenspaces_amd as de
+    d, n, k, rank = 512, 100, 200, 100
+    g = torch.Generator(device="cpu").manual_seed(5)
+    X = torch.randn(n, d, generator=g, dtype=torch.float64)
+    X *= torch.linspace(3.0, 1.0, d, dtype=torch.float64)  # a spread spectrum
+    S_h = (X.t() @ X / n).numpy()
+    S = torch.from_numpy(S_h).to(cuda)
+    for dtype in (torch.float64, torch.float32):
+        r = de.topk_eigh(S.to(dtype), k)
+        V = r.V.double().cpu().numpy()
+        ev = r.evals.double().cpu().numpy()
+        np.testing.assert_allclose(V.T @ V, np.eye(k), atol=2e-5)
+        w, Vr = ref_cpu.top_k_eigh(S_h, k)
+        lmax = w[-1]
+        assert ref_cpu.projector_distance(V[:, -rank:], Vr[:, -rank:]) <= P_TOL
+        np.testing.assert_allclose(ev[-rank:], w[-rank:], rtol=EV_TOL)
+        assert np.abs(ev[:k - rank]).max() <= 1e-5 * lmax
+        R = S_h @ V - V * ev
+        assert np.linalg.norm(R, axis=0).max() <= 1e-4 * lmax

@@ -52,58 +52,6 @@ def test_syrk_shapes(n, d, algo, cuda):
     _syrk_check(X, cuda, rel=tol, algo=algo)
 
 
-def test_syrk_split3_chunked_accumulation(cuda, monkeypatch):
-    """Split-pass variant (162) with a workspace that holds one 32-row chunk: it
-    then runs ceil(n/32) split + SYRK + diagonal-correction rounds accumulating
-    into S.  (The default fused variant needs no XP image and never chunks.)"""
-    monkeypatch.setenv("DEIG_SYRK_VARIANT", "162")
-    import ctypes
-    from distributed_eigenspaces_amd import _lib
-    L = _lib.lib()
-    rng = np.random.default_rng(11)
-    n, d = 1000, 300
-    X = (rng.standard_normal((n, d)) * 3 + 1).astype(np.float32)
-    x = torch.from_numpy(X).to(cuda)
-    S = torch.empty((d, d), dtype=torch.float32, device=cuda)
-    nbytes = L.deig_syrk_workspace_ex(32, d, _lib.DEIG_SYRK_SPLIT3)  # one 32-row chunk
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=cuda)
-    rc = L.deig_syrk_f32_ex(x.data_ptr(), n, d, d, ctypes.c_float(1.0 / n), S.data_ptr(), d,
-                            _lib.DEIG_SYRK_SPLIT3, ws.data_ptr(), nbytes,
-                            torch.cuda.current_stream().cuda_stream)
-    _lib.check(rc, "deig_syrk_f32_ex")
-    Sg = S.cpu().numpy().astype(np.float64)
-    Sr = ref_cpu.sigma_hat(X.astype(np.float64))
-    assert np.abs(Sg - Sr).max() <= 2e-6 * np.abs(Sr).max()
-    assert np.array_equal(Sg, Sg.T)
-    # too small a workspace is an error, not a silent fallback
-    rc = L.deig_syrk_f32_ex(x.data_ptr(), n, d, d, ctypes.c_float(1.0 / n), S.data_ptr(), d,
-                            _lib.DEIG_SYRK_SPLIT3, ws.data_ptr(), 1024,
-                            torch.cuda.current_stream().cuda_stream)
-    assert rc == _lib.DEIG_EWORKSPACE
-
-
-@pytest.mark.parametrize("n,d", [(1, 4), (33, 64), (1000, 520), (4097, 1000), (5000, 3072)])
-def test_syrk_fused_split_matches_split_pass(n, d, cuda, monkeypatch):
-    """The fused split (X staged as fp32 and split in LDS, variant 163, default)
-    forms the same bf16 pieces and MFMA sums as the split pass (162): equal up to
-    the order of the diagonal lo^2 correction sums."""
-    import distributed_eigenspaces_amd as de
-    rng = np.random.default_rng(n + 3 * d)
-    X = (rng.standard_normal((n, d)) * 2 + 0.5).astype(np.float32)
-    x = torch.from_numpy(X).to(cuda)
-    out = {}
-    for v in ("163", "162"):
-        monkeypatch.setenv("DEIG_SYRK_VARIANT", v)
-        out[v] = de.sigma_hat(x, algo="split3").cpu().numpy().astype(np.float64)
-    Sr = ref_cpu.sigma_hat(X.astype(np.float64))
-    scale = np.abs(Sr).max()
-    assert np.abs(out["163"] - Sr).max() <= _split3_tol(n) * scale
-    off = ~np.eye(d, dtype=bool)
-    assert np.array_equal(out["163"][off], out["162"][off]), "off-diagonal sums must be identical"
-    assert np.abs(np.diag(out["163"]) - np.diag(out["162"])).max() <= 1e-6 * scale
-    assert np.array_equal(out["163"], out["163"].T)
-
-
 def test_syrk_fused_split_strided_nan_padding(cuda):
     """Rows strided (ldx > d) with NaN in the padding columns and d not a multiple
     of the 256-feature panel: the fused split reads only features < d."""
