@@ -473,6 +473,569 @@ __device__ __forceinline__ void rr_small_body(const float* __restrict__ Cg, int 
   stamp(8);
 }
 
+// ---------------------------------------------------------------- small solve v2
+// The same generalised Rayleigh-Ritz step as rr_small_body (same outputs, same
+// decisions), restructured for the barrier / LDS-instruction budget of ONE
+// workgroup (r04: rr_small_body spent ~1.4 us per Jacobi step at p = 80 - 2 barriers
+// and ~40 LDS instructions per thread - and 2 x p barriers in the column-by-column
+// Cholesky and L^-1):
+//  * Cholesky of D M D and L^-1 in 16-column blocks: each 16 x 16 diagonal block is
+//    factored and inverted by one wave in registers (readlane broadcasts, no
+//    barrier), panels / trailing updates / block products are LDS-tiled products -
+//    ~4 barriers per block instead of 32;
+//  * Jacobi on the LOWER triangle only (half the block updates; stored with row
+//    stride p + 1 so column-strided accesses spread over the banks) and the
+//    eigenvector accumulator V held in REGISTERS: the round-robin ordering is the
+//    circle method, so the logical columns a pair slot holds move one slot per step in
+//    a fixed pattern (a-players down, b-players up); a row of V is split over 4 lanes
+//    (p / 8 slots each) that pass 2 values per step to their neighbours by shuffles.
+// Numerically: the Cholesky is right-looking by blocks (rounding order differs from
+// rr_small_body), the pivot floor and every later decision are the same.
+__device__ __forceinline__ float rdl(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// One wave: Cholesky of the 16 x 16 block at (o, o) of X1 (row stride p, already
+// updated by the earlier blocks), written back as L_JJ (lower; pivots floored as in
+// rr_small_body: v <= 1e-6 -> unit pivot, zero sub-diagonal); L_JJ^-1 written to the
+// diagonal block of X2 (row-major, zero upper) and to LS (16 x 17, row-major padded).
+__device__ __forceinline__ void chol16_wave(float* X1, float* X2, float* LS, int* flo, int p, int o,
+                                            int lane, int* info) {
+  float a[16];
+  const bool act = lane < 16;
+  const int row = act ? lane : 0;
+#pragma unroll
+  for (int j = 0; j < 16; j += 4) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(X1 + (o + row) * p + o + j);
+    a[j] = v[0];
+    a[j + 1] = v[1];
+    a[j + 2] = v[2];
+    a[j + 3] = v[3];
+  }
+  int nfl = 0;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const float v = rdl(a[c], c);
+    const bool floored = !(v > 1e-6f);
+    const float ljj = floored ? 1.0f : sqrtf(v);
+    nfl += floored ? 1 : 0;
+    if (lane == c) a[c] = ljj;
+    else if (lane > c) a[c] = floored ? 0.f : a[c] / ljj;
+    if (lane == 0) flo[o + c] = floored ? 1 : 0;
+#pragma unroll
+    for (int j = c + 1; j < 16; ++j) {
+      const float ljc = rdl(a[c], j);
+      if (lane >= j) a[j] = fmaf(-a[c], ljc, a[j]);
+    }
+  }
+  if (lane == 0 && nfl) info[0] += nfl;
+  // L_JJ^-1: lane j computes column j, x[i] = (delta_ij - sum_{t<i} l_it x_t) / l_ii
+  float x[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float s = (i == lane) ? 1.f : 0.f;
+#pragma unroll
+    for (int t = 0; t < i; ++t) s = fmaf(-rdl(a[t], i), x[t], s);
+    x[i] = (i >= lane) ? s / rdl(a[i], i) : 0.f;
+  }
+  if (act) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) X1[(o + lane) * p + o + j] = j <= lane ? a[j] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      X2[(o + t) * p + o + lane] = x[t];  // Linv[t][lane]
+      LS[t * 17 + lane] = x[t];
+    }
+  }
+}
+
+// 4 x 4 tile product acc += A[r0 + r][k] * B[k][c0 + c] over k in [k0, k1), A and B
+// row-major in LDS with row strides lda / ldb (16-B aligned rows).
+__device__ __forceinline__ void tile44(const float* A, int lda, const float* B, int ldb, int r0, int c0,
+                                       int k0, int k1, float (&acc)[4][4]) {
+  for (int k = k0; k < k1; k += 4) {
+    f32x4 ar[4], br[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ar[r] = *reinterpret_cast<const f32x4*>(A + (r0 + r) * lda + k);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) br[u] = *reinterpret_cast<const f32x4*>(B + (k + u) * ldb + c0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(ar[r][u], br[u][c], acc[r][c]);
+  }
+}
+
+// lower-triangle item idx -> (r, c), r >= c
+__device__ __forceinline__ void tri_rc(int idx, int& r, int& c) {
+  int t = (int)((sqrtf(8.f * (float)idx + 1.f) - 1.f) * 0.5f);
+  while ((t + 1) * (t + 2) / 2 <= idx) ++t;
+  while (t * (t + 1) / 2 > idx) --t;
+  r = t;
+  c = idx - t * (t + 1) / 2;
+}
+
+template <int NT>
+__device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int p,
+                                               float* __restrict__ Wout, float* __restrict__ lam_out,
+                                               float* __restrict__ cs_out, float* __restrict__ qs_out,
+                                               int* __restrict__ info, int max_jsweeps, float jrel) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int pp = p * p;
+  const int half = p >> 1;
+  const int nbk = p >> 4;
+  const int ldj = p + 1;  // Jacobi matrix row stride
+  const int ldp = p + 4;  // panel scratch row stride
+  float* X1 = sm;
+  float* X2 = sm + pp;         // p x (p + 1)
+  float* dsc = X2 + pp + p;    // p
+  float* lamv = dsc + p;       // p
+  float* gd = lamv + p;        // p
+  f32x4* rotp = reinterpret_cast<f32x4*>(gd + p);  // half records {c, s, a, b}
+  int* rank = reinterpret_cast<int*>(rotp + half);  // p
+  float* nq = reinterpret_cast<float*>(rank + p);   // p
+  int* flo = reinterpret_cast<int*>(nq + p);        // p
+  float* LS = reinterpret_cast<float*>(flo + p);    // 16 x 17 (+ 4 pad)
+  float* pan = LS + 16 * 17 + 4;                    // 16 x (p + 4)
+  float* red = pan + 16 * ldp;                      // NT / 64 + 2
+  int* nrot = reinterpret_cast<int*>(red + NT / 64 + 2);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ldc = 2 * p;
+  const float* Mg = Cg;
+  const float* Hg = Cg + p;
+  const float* Gg = Cg + (int64_t)p * ldc + p;
+  const uint64_t t0 = wall_clock64();
+  auto stamp = [&](int slot) {
+    if (tid == 0) info[slot] = (int)(wall_clock64() - t0);
+  };
+
+  // ---- 0. D = diag(M)^-1/2; X1 = D M D; X2 = 0
+  for (int a = tid; a < p; a += NT) {
+    const float m = Mg[a * ldc + a];
+    dsc[a] = (m > 0.f && isfinite(m)) ? rsqrtf(m) : 1.0f;
+  }
+  if (tid == 0) {
+    info[0] = 0;
+    info[1] = 0;
+    info[2] = 0;
+    info[3] = 0;
+  }
+  __syncthreads();
+  for (int idx = tid; idx < pp; idx += NT) {
+    const int a = idx / p, b = idx - a * p;
+    X1[idx] = Mg[a * ldc + b] * dsc[a] * dsc[b];
+    X2[idx] = 0.f;
+  }
+  __syncthreads();
+
+  // ---- 1. blocked Cholesky D M D = L L^T (lower, in X1), L_JJ^-1 into X2's diagonal
+  for (int J = 0; J < nbk; ++J) {
+    const int o = 16 * J;
+    if (wave == 0) chol16_wave(X1, X2, LS, flo, p, o, lane, info);
+    __syncthreads();
+    const int rem = p - o - 16;
+    if (rem <= 0) break;
+    // panel L_IJ = A_IJ L_JJ^-T (floored columns zero) -> pan[c][i], transposed
+    for (int it = tid; it < rem * 16; it += NT) {
+      const int c = it & 15, i = o + 16 + (it >> 4);
+      float s = 0.f;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) s = fmaf(X1[i * p + o + t], LS[c * 17 + t], s);
+      pan[c * ldp + i] = flo[o + c] ? 0.f : s;
+    }
+    __syncthreads();
+    // L_IJ into X1; trailing lower update A_II' -= L_IJ L_I'J^T (4 x 4 tiles)
+    for (int it = tid; it < rem * 16; it += NT) {
+      const int c = it & 15, i = o + 16 + (it >> 4);
+      X1[i * p + o + c] = pan[c * ldp + i];
+    }
+    const int nt = rem >> 2;
+    for (int it = tid; it < nt * (nt + 1) / 2; it += NT) {
+      int ti, tj;
+      tri_rc(it, ti, tj);
+      const int i0 = o + 16 + 4 * ti, j0 = o + 16 + 4 * tj;
+      float acc[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = 0.f;
+#pragma unroll 4
+      for (int c = 0; c < 16; ++c) {
+        const f32x4 li = *reinterpret_cast<const f32x4*>(pan + c * ldp + i0);
+        const f32x4 lj = *reinterpret_cast<const f32x4*>(pan + c * ldp + j0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) acc[r][cc] = fmaf(li[r], lj[cc], acc[r][cc]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        f32x4* dst = reinterpret_cast<f32x4*>(X1 + (i0 + r) * p + j0);
+        f32x4 v = *dst;
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) v[cc] -= acc[r][cc];
+        *dst = v;
+      }
+    }
+    __syncthreads();
+  }
+  stamp(4);
+
+  // ---- 2. L^-1 (lower) into X2 by block rows.  M_IK = L_II^-1 L_IK (K < I), stored
+  //         transposed in X1's (unused) upper triangle; then X_IJ = -sum_K M_IK X_KJ.
+  for (int it = tid; it < (nbk * (nbk - 1) / 2) * 16; it += NT) {
+    int I, K;
+    tri_rc(it >> 4, I, K);
+    I += 1;  // strictly lower blocks: (I, K) with I > K
+    const int tl = it & 15, i0 = 16 * I + 4 * (tl >> 2), j0 = 16 * K + 4 * (tl & 3);
+    float acc[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[r][c] = 0.f;
+    // Linv_II[i][t] (X2 diagonal block) x L_IK[t][j] (X1)
+    tile44(X2 + 16 * I, p, X1 + 16 * I * p, p, i0, j0, 0, 16, acc);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      f32x4 v{acc[0][c], acc[1][c], acc[2][c], acc[3][c]};
+      *reinterpret_cast<f32x4*>(X1 + (j0 + c) * p + i0) = v;  // M^T: row j, cols i (upper)
+    }
+  }
+  __syncthreads();
+  for (int I = 1; I < nbk; ++I) {
+    for (int it = tid; it < I * 16; it += NT) {
+      const int J = it >> 4, tl = it & 15;
+      const int i0 = 16 * I + 4 * (tl >> 2), j0 = 16 * J + 4 * (tl & 3);
+      float acc[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = 0.f;
+      for (int k = 16 * J; k < 16 * I; ++k) {
+        const f32x4 m = *reinterpret_cast<const f32x4*>(X1 + k * p + i0);  // M_I.[i0..i0+3][k]
+        const f32x4 xk = *reinterpret_cast<const f32x4*>(X2 + k * p + j0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(m[r], xk[c], acc[r][c]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        *reinterpret_cast<f32x4*>(X2 + (i0 + r) * p + j0) =
+            f32x4{-acc[r][0], -acc[r][1], -acc[r][2], -acc[r][3]};
+    }
+    __syncthreads();
+  }
+  stamp(5);
+
+  // ---- 3. X1 = D H D; T = L^-1 X1 stored transposed; X1 = L^-1 T^T = L^-1 H L^-T
+  for (int idx = tid; idx < pp; idx += NT) {
+    const int a = idx / p, b = idx - a * p;
+    X1[idx] = Hg[a * ldc + b] * dsc[a] * dsc[b];
+  }
+  __syncthreads();
+  const int nt4 = p >> 2;
+  for (int pass = 0; pass < 2; ++pass) {
+    constexpr int MAXT = (1024 + NT - 1) / NT;  // p <= 128: (p/4)^2 <= 1024 tiles
+    float acc[MAXT][4][4];
+#pragma unroll
+    for (int u = 0; u < MAXT; ++u) {
+      const int it = tid + u * NT;
+      if (it < nt4 * nt4) {
+        const int a0 = 4 * (it / nt4), b0 = 4 * (it % nt4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[u][r][c] = 0.f;
+        tile44(X2, p, X1, p, a0, b0, 0, a0 + 4, acc[u]);  // L^-1 lower: k <= a0 + 3
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < MAXT; ++u) {
+      const int it = tid + u * NT;
+      if (it < nt4 * nt4) {
+        const int a0 = 4 * (it / nt4), b0 = 4 * (it % nt4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (pass == 0) X1[(b0 + c) * p + a0 + r] = acc[u][r][c];
+            else X1[(a0 + r) * p + b0 + c] = acc[u][r][c];
+          }
+      }
+    }
+    __syncthreads();
+  }
+  stamp(6);
+
+  // ---- 4. Jacobi.  V = L^-T into registers (row r = tid / 4, quarter q = tid % 4,
+  //         slots [q m, q m + m), m = p / 8: the logical columns (a_t, b_t) of step 0:
+  //         slot 0 = (p - 1, 0), slot t >= 1 = (t, p - 1 - t)); H~ lower -> XJ.
+  constexpr int MS = 16;  // max slots per lane (p <= 128)
+  const int m = p >> 3;
+  const int vr = tid >> 2, vq = tid & 3, ts0 = vq * m;
+  const bool vact = vr < p;
+  float vA[MS], vB[MS];
+#pragma unroll
+  for (int u = 0; u < MS; ++u) {
+    const int t = ts0 + u;
+    const int ca = t == 0 ? p - 1 : t, cb = t == 0 ? 0 : p - 1 - t;
+    // X2 = L^-1 (lower): V = L^-T, V[r][c] = L^-1[c][r]
+    vA[u] = (vact && u < m) ? X2[ca * p + vr] : 0.f;
+    vB[u] = (vact && u < m) ? X2[cb * p + vr] : 0.f;
+  }
+  __syncthreads();
+  float* XJ = X2;  // (p x p, ld p + 1), lower triangle
+  for (int idx = tid; idx < pp; idx += NT) {
+    const int a = idx / p, b = idx - a * p;
+    if (b <= a) XJ[a * ldj + b] = 0.5f * (X1[a * p + b] + X1[b * p + a]);
+  }
+  if (tid == 0) {
+    nrot[1] = 0;
+    nrot[2] = 0;
+  }
+  // this thread's lower slot-block items (tr >= tc), fixed for the whole solve
+  constexpr int MI = (64 * 65 / 2 + NT - 1) / NT;
+  const int nitems = half * (half + 1) / 2;
+  int itr[MI], itc[MI];
+#pragma unroll
+  for (int u = 0; u < MI; ++u) {
+    const int it = tid + u * NT;
+    int r = 0, c = 0;
+    if (it < nitems) tri_rc(it, r, c);
+    itr[u] = r;
+    itc[u] = c;
+  }
+  __syncthreads();
+  auto XL = [&](int i, int j) -> float& { return i >= j ? XJ[i * ldj + j] : XJ[j * ldj + i]; };
+  for (int sw = 0; sw < max_jsweeps; ++sw) {
+    if (tid == 0) nrot[0] = 0;
+    float dmax = 0.f;
+    for (int a = tid; a < p; a += NT) dmax = fmaxf(dmax, fabsf(XJ[a * ldj + a]));
+    for (int o = 32; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o, 64));
+    if (lane == 0) red[wave] = dmax;
+    __syncthreads();
+    float amax = 0.f;
+    for (int i = 0; i < NT / 64; ++i) amax = fmaxf(amax, red[i]);
+    const float abs_thr = 1e-9f * amax;
+    {
+      int need = 0;
+      for (int idx = tid; idx < pp && !need; idx += NT) {
+        const int a = idx / p, b = idx - a * p;
+        if (b < a) {
+          const float apq = XJ[a * ldj + b];
+          need = fabsf(apq) > abs_thr &&
+                 fabsf(apq) > jrel * sqrtf(fabsf(XJ[a * ldj + a] * XJ[b * ldj + b]));
+        }
+      }
+      need = __syncthreads_or(need);
+      if (!need) {
+        if (tid == 0) info[3] = 1;
+        break;
+      }
+    }
+    for (int st = 0; st < p - 1; ++st) {
+      const int ci = 1 + (st & 1);
+      if (tid < half) {
+        int a, b;
+        if (tid == 0) {
+          a = p - 1;
+          b = st;
+        } else {
+          a = (st + tid) % (p - 1);
+          b = (st - tid + (p - 1)) % (p - 1);
+        }
+        const float app = XJ[a * ldj + a], aqq = XJ[b * ldj + b], apq = XL(a, b);
+        float c = 1.f, s = 0.f;
+        if (fabsf(apq) > abs_thr && fabsf(apq) > jrel * __builtin_amdgcn_sqrtf(fabsf(app * aqq))) {
+          rr_rot_cs(app, aqq, apq, c, s);
+          atomicAdd(nrot + ci, 1);
+        }
+        rotp[tid] = f32x4{c, s, __int_as_float(a), __int_as_float(b)};
+      }
+      __syncthreads();
+      const int step_rot = nrot[ci];
+      if (step_rot != 0) {
+        // lower slot blocks: rows (ar, br) of slot tr, columns (ac, bc) of slot tc
+#pragma unroll
+        for (int u = 0; u < MI; ++u) {
+          if (tid + u * NT < nitems) {
+            const int tr = itr[u], tc = itc[u];
+            const f32x4 qr = rotp[tr], qc = rotp[tc];
+            const int ar = __float_as_int(qr[2]), br = __float_as_int(qr[3]);
+            const int ac = __float_as_int(qc[2]), bc = __float_as_int(qc[3]);
+            const float cr = qr[0], sr = qr[1], cc = qc[0], sc = qc[1];
+            if (tr != tc) {
+              float& px = XL(ar, ac);
+              float& py = XL(ar, bc);
+              float& pz = XL(br, ac);
+              float& pw = XL(br, bc);
+              const float x = px, y = py, z = pz, w = pw;
+              const float x1 = cc * x - sc * y, y1 = sc * x + cc * y;
+              const float z1 = cc * z - sc * w, w1 = sc * z + cc * w;
+              px = cr * x1 - sr * z1;
+              pz = sr * x1 + cr * z1;
+              py = cr * y1 - sr * w1;
+              pw = sr * y1 + cr * w1;
+            } else {
+              float& px = XJ[ar * ldj + ar];
+              float& pw = XJ[br * ldj + br];
+              float& py = XL(ar, br);
+              const float x = px, y = py, w = pw;
+              const float x1 = cc * x - sc * y, y1 = sc * x + cc * y;
+              const float z1 = cc * y - sc * w, w1 = sc * y + cc * w;
+              px = cr * x1 - sr * z1;
+              py = cr * y1 - sr * w1;
+              pw = sr * y1 + cr * w1;
+            }
+          }
+        }
+      }
+      // V: rotate this lane's slots, then move to step st + 1's slots (a-players one
+      // slot down, b-players one slot up; slot 0's a is the fixed player p - 1)
+      if (vact) {
+        float nA[MS], nB[MS];
+#pragma unroll
+        for (int u = 0; u < MS; ++u) {
+          if (u < m) {
+            const f32x4 q = rotp[ts0 + u];
+            const float a = vA[u], b = vB[u];
+            nA[u] = q[0] * a - q[1] * b;
+            nB[u] = q[1] * a + q[0] * b;
+          }
+        }
+        const float sendDown = nA[0], sendUp = nB[m - 1];
+        const float fromUp = __shfl_down(sendDown, 1, 4);  // lane q + 1's nA[0]
+        const float fromDown = __shfl_up(sendUp, 1, 4);    // lane q - 1's nB[m - 1]
+#pragma unroll
+        for (int u = 0; u < MS; ++u) {
+          if (u + 1 < m) vA[u] = nA[u + 1];
+          if (u >= 1 && u < m) vB[u] = nB[u - 1];
+        }
+        vA[m - 1] = (vq == 3) ? nB[m - 1] : fromUp;  // slot h - 1: a <- its own b
+        vB[0] = fromDown;
+        if (vq == 0) {  // slot 0: a is the fixed player, b <- slot 1's a
+          vA[0] = nA[0];
+          vB[0] = nA[1];
+        }
+      }
+      __syncthreads();
+      if (tid == 0) {
+        nrot[0] += step_rot;
+        nrot[ci] = 0;
+      }
+    }
+    __syncthreads();
+    const int swrot = nrot[0];
+    if (tid == 0) {
+      info[1] = sw + 1;
+      info[2] += swrot;
+    }
+    __syncthreads();
+    if (swrot == 0) {
+      if (tid == 0) info[3] = 1;
+      break;
+    }
+  }
+
+  stamp(7);
+  // ---- 5. eigenvalues; V (full sweeps: back at step 0's slots) -> X1 = W = D V
+  for (int a = tid; a < p; a += NT) lamv[a] = XJ[a * ldj + a];
+  if (vact) {
+#pragma unroll
+    for (int u = 0; u < MS; ++u) {
+      if (u < m) {
+        const int t = ts0 + u;
+        const int ca = t == 0 ? p - 1 : t, cb = t == 0 ? 0 : p - 1 - t;
+        X1[vr * p + ca] = vA[u] * dsc[vr];
+        X1[vr * p + cb] = vB[u] * dsc[vr];
+      }
+    }
+  }
+  __syncthreads();
+  float* Wm = X1;   // W = D L^-T U
+  float* Ts = X2;   // scratch (ld p)
+  for (int idx = tid; idx < pp; idx += NT) {
+    const int a = idx / p, b = idx - a * p;
+    Ts[idx] = Gg[a * ldc + b];
+  }
+  __syncthreads();
+  // ---- 6. g_j = w_j^T G w_j, n_j = w_j^T M w_j: column sums of (G W) .* W, (M W) .* W
+  for (int pass = 0; pass < 2; ++pass) {
+    constexpr int MAXT = (1024 + NT - 1) / NT;
+    float acc[MAXT][4][4];
+#pragma unroll
+    for (int u = 0; u < MAXT; ++u) {
+      const int it = tid + u * NT;
+      if (it < nt4 * nt4) {
+        const int a0 = 4 * (it / nt4), b0 = 4 * (it % nt4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[u][r][c] = 0.f;
+        tile44(Ts, p, Wm, p, a0, b0, 0, p, acc[u]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < MAXT; ++u) {
+      const int it = tid + u * NT;
+      if (it < nt4 * nt4) {
+        const int a0 = 4 * (it / nt4), b0 = 4 * (it % nt4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) Ts[(a0 + r) * p + b0 + c] = acc[u][r][c] * Wm[(a0 + r) * p + b0 + c];
+      }
+    }
+    __syncthreads();
+    float* dst = pass == 0 ? gd : nq;
+    for (int j = tid; j < p; j += NT) {
+      float s = 0.f;
+      for (int a = 0; a < p; ++a) s += Ts[a * p + j];
+      dst[j] = s;
+    }
+    __syncthreads();
+    if (pass == 0) {
+      for (int idx = tid; idx < pp; idx += NT) {
+        const int a = idx / p, b = idx - a * p;
+        Ts[idx] = Mg[a * ldc + b];
+      }
+      __syncthreads();
+    }
+  }
+  for (int j = tid; j < p; j += NT) {
+    const float lj = lamv[j];
+    int rk = 0;
+    for (int b = 0; b < p; ++b) {
+      const float lb = lamv[b];
+      rk += (lb > lj || (lb == lj && b < j)) ? 1 : 0;
+    }
+    rank[j] = rk;
+  }
+  if (tid == 0) {
+    float mx = 0.f;
+    for (int j = 0; j < p; ++j) mx = fmaxf(mx, gd[j]);
+    red[0] = mx;
+  }
+  __syncthreads();
+  const float gthr = red[0] * 1e-10f;
+  for (int j = tid; j < p; j += NT) {
+    const int rk = rank[j];
+    lam_out[rk] = lamv[j];
+    cs_out[rk] = (gd[j] > gthr && gd[j] > 0.f) ? rsqrtf(gd[j]) : 0.f;
+    qs_out[rk] = (nq[j] > 1e-30f && isfinite(nq[j])) ? rsqrtf(nq[j]) : 1.f;
+  }
+  for (int idx = tid; idx < pp; idx += NT) {
+    const int a = idx / p, j = idx - a * p;
+    Wout[a * p + rank[j]] = Wm[idx];
+  }
+  stamp(8);
+}
+
 template <int NT>
 __global__ __launch_bounds__(NT) void rr_small_kernel(const float* __restrict__ Cg, int p,
                                                       float* __restrict__ Wout,
@@ -482,6 +1045,17 @@ __global__ __launch_bounds__(NT) void rr_small_kernel(const float* __restrict__ 
                                                       int* __restrict__ info, int max_jsweeps,
                                                       float jrel) {
   rr_small_body<NT>(Cg, p, Wout, lam_out, cs_out, qs_out, info, max_jsweeps, jrel);
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void rr_small2_kernel(const float* __restrict__ Cg, int p,
+                                                       float* __restrict__ Wout,
+                                                       float* __restrict__ lam_out,
+                                                       float* __restrict__ cs_out,
+                                                       float* __restrict__ qs_out,
+                                                       int* __restrict__ info, int max_jsweeps,
+                                                       float jrel) {
+  rr_small2_body<NT>(Cg, p, Wout, lam_out, cs_out, qs_out, info, max_jsweeps, jrel);
 }
 
 // Up to kRRBatch independent small solves in one launch, one workgroup each (the
@@ -500,6 +1074,12 @@ template <int NT>
 __global__ __launch_bounds__(NT) void rr_small_batch_kernel(RRBatchArgs a, int p, float jrel) {
   const int i = blockIdx.x;
   rr_small_body<NT>(a.C[i], p, a.W[i], a.lam[i], a.cs[i], a.qs[i], a.info[i], a.max_jsweeps[i], jrel);
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void rr_small2_batch_kernel(RRBatchArgs a, int p, float jrel) {
+  const int i = blockIdx.x;
+  rr_small2_body<NT>(a.C[i], p, a.W[i], a.lam[i], a.cs[i], a.qs[i], a.info[i], a.max_jsweeps[i], jrel);
 }
 
 __global__ __launch_bounds__(256) void rr_update_kernel(float* __restrict__ Z, int64_t d, int p,
@@ -893,6 +1473,11 @@ size_t rr_small_shm(int p) {
   return (size_t)(2 * p * p + 7 * p + RT / 64 + 20) * sizeof(float);
 }
 
+constexpr int RT2 = 512;  // rr_small2: 4 lanes per row of V for p <= 128
+size_t rr_small2_shm(int p) {
+  return (size_t)(2 * p * p + 9 * p + 16 * 17 + 4 + 16 * (p + 4) + RT2 / 64 + 2 + 4) * sizeof(float);
+}
+
 }  // namespace
 
 int rr_init_launch(float* Z, int64_t d, int p, const float* Q0, int k0, int64_t ldq0,
@@ -905,7 +1490,16 @@ int rr_init_launch(float* Z, int64_t d, int p, const float* Q0, int k0, int64_t 
 }
 
 int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream, int max_jsweeps, float jrel) {
-  DEIG_REQUIRE(p >= 4 && p <= 128 && p % 4 == 0, "rr_small: p=%d out of range", p);
+  DEIG_REQUIRE(p >= 16 && p <= 128 && p % 16 == 0, "rr_small: p=%d out of range", p);
+#ifndef DEIG_AB_RR_V1
+  static const hipError_t attr2 = hipFuncSetAttribute(
+      (const void*)rr_small2_kernel<RT2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rr_small2_shm(128));
+  DEIG_HIP_CHECK(attr2);
+  hipLaunchKernelGGL(rr_small2_kernel<RT2>, dim3(1), dim3(RT2), rr_small2_shm(p), stream, b.C, p, b.W, b.lam,
+                     b.cs, b.qs, b.info, max_jsweeps, jrel);
+  DEIG_HIP_CHECK(hipGetLastError());
+  return DEIG_OK;
+#endif
   const size_t shm = rr_small_shm(p);
   // once per process (C++11 thread-safe static initialisation)
   static const hipError_t attr = hipFuncSetAttribute(
@@ -923,7 +1517,13 @@ int rr_small_launch(const RRBuffers& b, int p, hipStream_t stream, int max_jswee
 
 int rr_small_batch_launch(const RRBuffers* const* bs, const int* max_jsweeps, int n, int p,
                           hipStream_t stream, float jrel) {
-  DEIG_REQUIRE(p >= 4 && p <= 128 && p % 4 == 0, "rr_small: p=%d out of range", p);
+  DEIG_REQUIRE(p >= 16 && p <= 128 && p % 16 == 0, "rr_small: p=%d out of range", p);
+#ifndef DEIG_AB_RR_V1
+  static const hipError_t attr2 = hipFuncSetAttribute(
+      (const void*)rr_small2_batch_kernel<RT2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (int)rr_small2_shm(128));
+  DEIG_HIP_CHECK(attr2);
+#endif
   static const hipError_t attr = hipFuncSetAttribute(
       (const void*)rr_small_batch_kernel<RT>, hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)rr_small_shm(128));
@@ -941,7 +1541,11 @@ int rr_small_batch_launch(const RRBuffers* const* bs, const int* max_jsweeps, in
       a.info[i] = b.info;
       a.max_jsweeps[i] = max_jsweeps[i0 + i];
     }
+#ifndef DEIG_AB_RR_V1
+    hipLaunchKernelGGL(rr_small2_batch_kernel<RT2>, dim3(m), dim3(RT2), rr_small2_shm(p), stream, a, p, jrel);
+#else
     hipLaunchKernelGGL(rr_small_batch_kernel<RT>, dim3(m), dim3(RT), rr_small_shm(p), stream, a, p, jrel);
+#endif
     DEIG_HIP_CHECK(hipGetLastError());
   }
   return DEIG_OK;
