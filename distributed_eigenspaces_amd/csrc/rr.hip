@@ -907,15 +907,19 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
             nB[u] = q[1] * a + q[0] * b;
           }
         }
-        const float sendDown = nA[0], sendUp = nB[m - 1];
-        const float fromUp = __shfl_down(sendDown, 1, 4);  // lane q + 1's nA[0]
-        const float fromDown = __shfl_up(sendUp, 1, 4);    // lane q - 1's nB[m - 1]
+        // (no register array is indexed by the runtime m: selects over static indices)
+        float lastB = nB[0];
+#pragma unroll
+        for (int u = 1; u < MS; ++u) lastB = (u == m - 1) ? nB[u] : lastB;
+        const float fromUp = __shfl_down(nA[0], 1, 4);  // lane q + 1's nA[0]
+        const float fromDown = __shfl_up(lastB, 1, 4);  // lane q - 1's nB[m - 1]
+        const float tailA = (vq == 3) ? lastB : fromUp;  // slot h - 1: a <- its own b
 #pragma unroll
         for (int u = 0; u < MS; ++u) {
-          if (u + 1 < m) vA[u] = nA[u + 1];
-          if (u >= 1 && u < m) vB[u] = nB[u - 1];
+          const float na = (u + 1 < MS) ? nA[u + 1 < MS ? u + 1 : u] : 0.f;
+          vA[u] = (u == m - 1) ? tailA : na;
+          if (u >= 1) vB[u] = nB[u - 1];
         }
-        vA[m - 1] = (vq == 3) ? nB[m - 1] : fromUp;  // slot h - 1: a <- its own b
         vB[0] = fromDown;
         if (vq == 0) {  // slot 0: a is the fixed player, b <- slot 1's a
           vA[0] = nA[0];
