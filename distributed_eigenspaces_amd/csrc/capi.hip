@@ -441,6 +441,9 @@ struct Solver {
     // (eigenvalues clustered near 1) 3 above 1e-2 (the tighter cap cost config 4's
     // aggregation 2.05 -> 2.65 ms).
     jcap_sweeps = o.jcap_sweeps >= 0 ? o.jcap_sweeps : (op.implicit ? 3 : 2);
+    // a basis spanning the whole space (tiny d, k close to d): the first Rayleigh-Ritz
+    // step is the exact eigendecomposition - run its Jacobi to convergence
+    if (pb >= d) jcap_sweeps = 0;
     jcap_above = o.jcap_above >= 0.f ? o.jcap_above : (op.implicit ? 1e-2f : 1e-4f);
     fuse = w.sweep_ws != nullptr;
     best = 3.4e38f;
@@ -917,7 +920,9 @@ struct SolveSM {
     // Indefinite S: the most negative Ritz value of the block against the block's
     // target (and the operator's scale - deflation residue is ~1e-7 of it).
     const float tmin = sv.lam_h[pb - 1];
-    if (!op0.implicit && attempt < kMaxShifts &&
+    // (a basis spanning the whole space needs no shift: its Rayleigh-Ritz step is exact,
+    // no power or filter step ever ranked |lambda|)
+    if (!op0.implicit && attempt < kMaxShifts && pb < d &&
         tmin < -fmaxf(kNegRel * scale, kNegTarget * fmaxf(sv.lam_h[kc - 1], 0.f))) {
       shift = kShiftGrow * (shift - (double)tmin);  // |theta_min| of the shifted op
       if (sv.o.debug)

@@ -82,9 +82,16 @@ __global__ __launch_bounds__(256) void shift_finalize_kernel(const float* __rest
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= d * d) return;
   const int64_t i = idx / d, j = idx - i * d;
+  // every expression symmetric in (i, j): + and * commute, Sc is bit-symmetric.
+  // No contraction: fused into fma(sv_i, mu_j, mu_i sv_j) the cross term would round
+  // differently for (j, i) - r03's float64 Sigma was not bit-symmetric
+  // (tests/test_gpu_integration_stub.py).
   const double mi = mu[i], mj = mu[j];
-  // every expression symmetric in (i, j): + and * commute, Sc is bit-symmetric
-  const double cross = sv[i] * mj + mi * sv[j];
+  double cross;
+  {
+#pragma clang fp contract(off)
+    cross = sv[i] * mj + mi * sv[j];
+  }
   const double v = (double)Sc[i * ldc + j] + alpha * (cross + n * (mi * mj));
   if (S64) S64[i * lds64 + j] = v;
   if (S) S[i * lds + j] = (float)v;

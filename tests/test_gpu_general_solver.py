@@ -131,8 +131,8 @@ def test_indefinite_padded_dimension(d, k, case, cuda):
     the start basis has zero padding rows; d = 10 / 13 / 20: the basis spans the padded
     space, whose diagonal is set below S's spectrum."""
     import distributed_eigenspaces_amd as de
-    if case == "negative_definite":
-        lam = -np.linspace(1.0, 40.0, d)
+    if case == "negative_definite":  # a clear gap below the top k, like the other planted cases
+        lam = -np.concatenate([np.linspace(1.0, 2.0, k), np.linspace(4.0, 40.0, d - k)])
     else:  # top k straddle zero, most of the spectrum negative
         lam = np.concatenate([np.linspace(2.0, 1.0, k // 2), -np.linspace(0.5, 1.5, k - k // 2),
                               -np.linspace(3.0, 30.0, d - k)])
