@@ -586,7 +586,6 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
   const int pp = p * p;
   const int half = p >> 1;
   const int nbk = p >> 4;
-  const int ldj = p + 1;  // Jacobi matrix row stride
   const int ldp = p + 4;  // panel scratch row stride
   float* X1 = sm;
   float* X2 = sm + pp;         // p x (p + 1)
@@ -788,15 +787,17 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
     vB[u] = (vact && u < m) ? X2[cb * p + vr] : 0.f;
   }
   __syncthreads();
-  float* XJ = X2;  // (p x p, ld p + 1), lower triangle
+  // H~'s lower triangle, packed (pk), twice: every step reads buffer A and writes
+  // buffer B (one barrier per step: no thread's write can overtake another's read).
+  const int nlow = p * (p + 1) / 2;
+  float* XJa = X2;
+  float* XJb = X2 + nlow;  // X2 holds p^2 + p floats = 2 nlow
+  auto pk = [](int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; };
   for (int idx = tid; idx < pp; idx += NT) {
     const int a = idx / p, b = idx - a * p;
-    if (b <= a) XJ[a * ldj + b] = 0.5f * (X1[a * p + b] + X1[b * p + a]);
+    if (b <= a) XJa[a * (a + 1) / 2 + b] = 0.5f * (X1[a * p + b] + X1[b * p + a]);
   }
-  if (tid == 0) {
-    nrot[1] = 0;
-    nrot[2] = 0;
-  }
+  if (tid == 0) nrot[0] = 0;
   // this thread's lower slot-block items (tr >= tc), fixed for the whole solve
   constexpr int MI = (64 * 65 / 2 + NT - 1) / NT;
   const int nitems = half * (half + 1) / 2;
@@ -810,11 +811,23 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
     itc[u] = c;
   }
   __syncthreads();
-  auto XL = [&](int i, int j) -> float& { return i >= j ? XJ[i * ldj + j] : XJ[j * ldj + i]; };
+  // slot t's logical pair at step st (circle method; slot 0 = (p - 1, st))
+  auto slot_a = [&](int st, int t) {
+    int x = st + t;
+    if (x >= p - 1) x -= p - 1;
+    return t == 0 ? p - 1 : x;
+  };
+  auto slot_b = [&](int st, int t) {
+    int x = st - t;
+    if (x < 0) x += p - 1;
+    return x;
+  };
+  float* XA = XJa;
+  float* XB = XJb;
+  int swrot_acc = 0;  // wave 0, lane 0: rotations of the sweep
   for (int sw = 0; sw < max_jsweeps; ++sw) {
-    if (tid == 0) nrot[0] = 0;
     float dmax = 0.f;
-    for (int a = tid; a < p; a += NT) dmax = fmaxf(dmax, fabsf(XJ[a * ldj + a]));
+    for (int a = tid; a < p; a += NT) dmax = fmaxf(dmax, fabsf(XA[a * (a + 1) / 2 + a]));
     for (int o = 32; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o, 64));
     if (lane == 0) red[wave] = dmax;
     __syncthreads();
@@ -826,9 +839,9 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
       for (int idx = tid; idx < pp && !need; idx += NT) {
         const int a = idx / p, b = idx - a * p;
         if (b < a) {
-          const float apq = XJ[a * ldj + b];
+          const float apq = XA[a * (a + 1) / 2 + b];
           need = fabsf(apq) > abs_thr &&
-                 fabsf(apq) > jrel * sqrtf(fabsf(XJ[a * ldj + a] * XJ[b * ldj + b]));
+                 fabsf(apq) > jrel * sqrtf(fabsf(XA[a * (a + 1) / 2 + a] * XA[b * (b + 1) / 2 + b]));
         }
       }
       need = __syncthreads_or(need);
@@ -837,75 +850,64 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
         break;
       }
     }
+    swrot_acc = 0;
     for (int st = 0; st < p - 1; ++st) {
-      const int ci = 1 + (st & 1);
-      if (tid < half) {
-        int a, b;
-        if (tid == 0) {
-          a = p - 1;
-          b = st;
-        } else {
-          a = (st + tid) % (p - 1);
-          b = (st - tid + (p - 1)) % (p - 1);
-        }
-        const float app = XJ[a * ldj + a], aqq = XJ[b * ldj + b], apq = XL(a, b);
-        float c = 1.f, s = 0.f;
+      // every wave computes all half rotations of the step (lane t: slot t) from A -
+      // redundantly, so nothing waits on another wave; items and V fetch theirs
+      // by lane shuffles
+      float rc = 1.f, rs = 0.f;
+      int rot = 0;
+      if (lane < half) {
+        const int a = slot_a(st, lane), b = slot_b(st, lane);
+        const float app = XA[pk(a, a)], aqq = XA[pk(b, b)], apq = XA[pk(a, b)];
         if (fabsf(apq) > abs_thr && fabsf(apq) > jrel * __builtin_amdgcn_sqrtf(fabsf(app * aqq))) {
-          rr_rot_cs(app, aqq, apq, c, s);
-          atomicAdd(nrot + ci, 1);
+          rr_rot_cs(app, aqq, apq, rc, rs);
+          rot = 1;
         }
-        rotp[tid] = f32x4{c, s, __int_as_float(a), __int_as_float(b)};
       }
-      __syncthreads();
-      const int step_rot = nrot[ci];
-      if (step_rot != 0) {
-        // lower slot blocks: rows (ar, br) of slot tr, columns (ac, bc) of slot tc
+      if (wave == 0) {
+        const uint64_t bal = __ballot(rot);
+        swrot_acc += __popcll(bal);
+      }
 #pragma unroll
-        for (int u = 0; u < MI; ++u) {
-          if (tid + u * NT < nitems) {
-            const int tr = itr[u], tc = itc[u];
-            const f32x4 qr = rotp[tr], qc = rotp[tc];
-            const int ar = __float_as_int(qr[2]), br = __float_as_int(qr[3]);
-            const int ac = __float_as_int(qc[2]), bc = __float_as_int(qc[3]);
-            const float cr = qr[0], sr = qr[1], cc = qc[0], sc = qc[1];
-            if (tr != tc) {
-              float& px = XL(ar, ac);
-              float& py = XL(ar, bc);
-              float& pz = XL(br, ac);
-              float& pw = XL(br, bc);
-              const float x = px, y = py, z = pz, w = pw;
-              const float x1 = cc * x - sc * y, y1 = sc * x + cc * y;
-              const float z1 = cc * z - sc * w, w1 = sc * z + cc * w;
-              px = cr * x1 - sr * z1;
-              pz = sr * x1 + cr * z1;
-              py = cr * y1 - sr * w1;
-              pw = sr * y1 + cr * w1;
-            } else {
-              float& px = XJ[ar * ldj + ar];
-              float& pw = XJ[br * ldj + br];
-              float& py = XL(ar, br);
-              const float x = px, y = py, w = pw;
-              const float x1 = cc * x - sc * y, y1 = sc * x + cc * y;
-              const float z1 = cc * y - sc * w, w1 = sc * y + cc * w;
-              px = cr * x1 - sr * z1;
-              py = cr * y1 - sr * w1;
-              pw = sr * y1 + cr * w1;
-            }
+      for (int u = 0; u < MI; ++u) {
+        const int tr = itr[u], tc = itc[u];
+        const float cr = __shfl(rc, tr), sr = __shfl(rs, tr);
+        const float cc = __shfl(rc, tc), sc = __shfl(rs, tc);
+        if (tid + u * NT < nitems) {
+          const int ar = slot_a(st, tr), br = slot_b(st, tr);
+          if (tr != tc) {
+            const int ac = slot_a(st, tc), bc = slot_b(st, tc);
+            const int ixx = pk(ar, ac), ixy = pk(ar, bc), ixz = pk(br, ac), ixw = pk(br, bc);
+            const float x = XA[ixx], y = XA[ixy], z = XA[ixz], w = XA[ixw];
+            const float x1 = cc * x - sc * y, y1 = sc * x + cc * y;
+            const float z1 = cc * z - sc * w, w1 = sc * z + cc * w;
+            XB[ixx] = cr * x1 - sr * z1;
+            XB[ixz] = sr * x1 + cr * z1;
+            XB[ixy] = cr * y1 - sr * w1;
+            XB[ixw] = sr * y1 + cr * w1;
+          } else {
+            const int ixx = pk(ar, ar), ixw = pk(br, br), ixy = pk(ar, br);
+            const float x = XA[ixx], y = XA[ixy], w = XA[ixw];
+            const float x1 = cc * x - sc * y, y1 = sc * x + cc * y;
+            const float z1 = cc * y - sc * w, w1 = sc * y + cc * w;
+            XB[ixx] = cr * x1 - sr * z1;
+            XB[ixy] = cr * y1 - sr * w1;
+            XB[ixw] = sr * y1 + cr * w1;
           }
         }
       }
       // V: rotate this lane's slots, then move to step st + 1's slots (a-players one
       // slot down, b-players one slot up; slot 0's a is the fixed player p - 1)
-      if (vact) {
+      {
         float nA[MS], nB[MS];
 #pragma unroll
         for (int u = 0; u < MS; ++u) {
-          if (u < m) {
-            const f32x4 q = rotp[ts0 + u];
-            const float a = vA[u], b = vB[u];
-            nA[u] = q[0] * a - q[1] * b;
-            nB[u] = q[1] * a + q[0] * b;
-          }
+          const int src = ts0 + (u < m ? u : 0);
+          const float c = __shfl(rc, src), sn = __shfl(rs, src);
+          const float a = vA[u], b = vB[u];
+          nA[u] = c * a - sn * b;
+          nB[u] = sn * a + c * b;
         }
         // (no register array is indexed by the runtime m: selects over static indices)
         float lastB = nB[0];
@@ -926,12 +928,12 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
           vB[0] = nA[1];
         }
       }
+      float* t = XA;
+      XA = XB;
+      XB = t;
       __syncthreads();
-      if (tid == 0) {
-        nrot[0] += step_rot;
-        nrot[ci] = 0;
-      }
     }
+    if (tid == 0) nrot[0] = swrot_acc;
     __syncthreads();
     const int swrot = nrot[0];
     if (tid == 0) {
@@ -947,7 +949,7 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
 
   stamp(7);
   // ---- 5. eigenvalues; V (full sweeps: back at step 0's slots) -> X1 = W = D V
-  for (int a = tid; a < p; a += NT) lamv[a] = XJ[a * ldj + a];
+  for (int a = tid; a < p; a += NT) lamv[a] = XA[a * (a + 1) / 2 + a];
   if (vact) {
 #pragma unroll
     for (int u = 0; u < MS; ++u) {
