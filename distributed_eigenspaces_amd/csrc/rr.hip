@@ -770,64 +770,34 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
   }
   stamp(6);
 
-  // ---- 4. Jacobi.  V = L^-T into registers (row r = tid / 4, quarter q = tid % 4,
-  //         slots [q m, q m + m), m = p / 8: the logical columns (a_t, b_t) of step 0:
-  //         slot 0 = (p - 1, 0), slot t >= 1 = (t, p - 1 - t)); H~ lower -> XJ.
-  constexpr int MS = 16;  // max slots per lane (p <= 128)
-  const int m = p >> 3;
-  const int vr = tid >> 2, vq = tid & 3, ts0 = vq * m;
-  const bool vact = vr < p;
-  float vA[MS], vB[MS];
-#pragma unroll
-  for (int u = 0; u < MS; ++u) {
-    const int t = ts0 + u;
-    const int ca = t == 0 ? p - 1 : t, cb = t == 0 ? 0 : p - 1 - t;
-    // X2 = L^-1 (lower): V = L^-T, V[r][c] = L^-1[c][r]
-    vA[u] = (vact && u < m) ? X2[ca * p + vr] : 0.f;
-    vB[u] = (vact && u < m) ? X2[cb * p + vr] : 0.f;
-  }
-  __syncthreads();
-  // H~'s lower triangle, packed (pk), twice: every step reads buffer A and writes
-  // buffer B (one barrier per step: no thread's write can overtake another's read).
-  const int nlow = p * (p + 1) / 2;
-  float* XJa = X2;
-  float* XJb = X2 + nlow;  // X2 holds p^2 + p floats = 2 nlow
-  auto pk = [](int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; };
+  // ---- 4. Jacobi (rr_small_body's: full storage, round-robin pairs, 2 barriers per
+  //         step; r04 A/B: every restructured step measured slower - V in registers
+  //         moved along the circle method, lower-triangle storage, rotations per wave
+  //         by shuffles - their extra VALU / shuffle issue cost more than the LDS
+  //         traffic they saved, profiles/r04d_rr_phases.log).
+  //         symmetrise H~; X2 = L^-1 -> the eigenvector accumulator V0 = L^-T
   for (int idx = tid; idx < pp; idx += NT) {
     const int a = idx / p, b = idx - a * p;
-    if (b <= a) XJa[a * (a + 1) / 2 + b] = 0.5f * (X1[a * p + b] + X1[b * p + a]);
+    if (a < b) {
+      const float v = 0.5f * (X1[a * p + b] + X1[b * p + a]);
+      X1[a * p + b] = v;
+      X1[b * p + a] = v;
+      const float l = X2[b * p + a];
+      X2[a * p + b] = l;
+      X2[b * p + a] = 0.f;
+    }
   }
-  if (tid == 0) nrot[0] = 0;
-  // this thread's lower slot-block items (tr >= tc), fixed for the whole solve
-  constexpr int MI = (64 * 65 / 2 + NT - 1) / NT;
-  const int nitems = half * (half + 1) / 2;
-  int itr[MI], itc[MI];
-#pragma unroll
-  for (int u = 0; u < MI; ++u) {
-    const int it = tid + u * NT;
-    int r = 0, c = 0;
-    if (it < nitems) tri_rc(it, r, c);
-    itr[u] = r;
-    itc[u] = c;
+  if (tid == 0) {
+    nrot[1] = 0;
+    nrot[2] = 0;
   }
   __syncthreads();
-  // slot t's logical pair at step st (circle method; slot 0 = (p - 1, st))
-  auto slot_a = [&](int st, int t) {
-    int x = st + t;
-    if (x >= p - 1) x -= p - 1;
-    return t == 0 ? p - 1 : x;
-  };
-  auto slot_b = [&](int st, int t) {
-    int x = st - t;
-    if (x < 0) x += p - 1;
-    return x;
-  };
-  float* XA = XJa;
-  float* XB = XJb;
-  int swrot_acc = 0;  // wave 0, lane 0: rotations of the sweep
+  const int tr0 = tid / half, tc0 = tid - tr0 * half;
+  const int dq = NT / half, dr = NT - dq * half;
   for (int sw = 0; sw < max_jsweeps; ++sw) {
+    if (tid == 0) nrot[0] = 0;
     float dmax = 0.f;
-    for (int a = tid; a < p; a += NT) dmax = fmaxf(dmax, fabsf(XA[a * (a + 1) / 2 + a]));
+    for (int a = tid; a < p; a += NT) dmax = fmaxf(dmax, fabsf(X1[a * p + a]));
     for (int o = 32; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o, 64));
     if (lane == 0) red[wave] = dmax;
     __syncthreads();
@@ -839,9 +809,8 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
       for (int idx = tid; idx < pp && !need; idx += NT) {
         const int a = idx / p, b = idx - a * p;
         if (b < a) {
-          const float apq = XA[a * (a + 1) / 2 + b];
-          need = fabsf(apq) > abs_thr &&
-                 fabsf(apq) > jrel * sqrtf(fabsf(XA[a * (a + 1) / 2 + a] * XA[b * (b + 1) / 2 + b]));
+          const float apq = X1[a * p + b];
+          need = fabsf(apq) > abs_thr && fabsf(apq) > jrel * sqrtf(fabsf(X1[a * p + a] * X1[b * p + b]));
         }
       }
       need = __syncthreads_or(need);
@@ -850,90 +819,73 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
         break;
       }
     }
-    swrot_acc = 0;
     for (int st = 0; st < p - 1; ++st) {
-      // every wave computes all half rotations of the step (lane t: slot t) from A -
-      // redundantly, so nothing waits on another wave; items and V fetch theirs
-      // by lane shuffles
-      float rc = 1.f, rs = 0.f;
-      int rot = 0;
-      if (lane < half) {
-        const int a = slot_a(st, lane), b = slot_b(st, lane);
-        const float app = XA[pk(a, a)], aqq = XA[pk(b, b)], apq = XA[pk(a, b)];
-        if (fabsf(apq) > abs_thr && fabsf(apq) > jrel * __builtin_amdgcn_sqrtf(fabsf(app * aqq))) {
-          rr_rot_cs(app, aqq, apq, rc, rs);
-          rot = 1;
+      const int ci = 1 + (st & 1);
+      if (tid < half) {
+        int a, b;
+        if (tid == 0) {
+          a = p - 1;
+          b = st;
+        } else {
+          a = (st + tid) % (p - 1);
+          b = (st - tid + (p - 1)) % (p - 1);
         }
+        const float app = X1[a * p + a], aqq = X1[b * p + b], apq = X1[a * p + b];
+        float c = 1.f, s = 0.f;
+        if (fabsf(apq) > abs_thr && fabsf(apq) > jrel * __builtin_amdgcn_sqrtf(fabsf(app * aqq))) {
+          rr_rot_cs(app, aqq, apq, c, s);
+          atomicAdd(nrot + ci, 1);
+        }
+        rotp[tid] = f32x4{c, s, __int_as_float(a), __int_as_float(b)};
       }
-      if (wave == 0) {
-        const uint64_t bal = __ballot(rot);
-        swrot_acc += __popcll(bal);
-      }
-#pragma unroll
-      for (int u = 0; u < MI; ++u) {
-        const int tr = itr[u], tc = itc[u];
-        const float cr = __shfl(rc, tr), sr = __shfl(rs, tr);
-        const float cc = __shfl(rc, tc), sc = __shfl(rs, tc);
-        if (tid + u * NT < nitems) {
-          const int ar = slot_a(st, tr), br = slot_b(st, tr);
-          if (tr != tc) {
-            const int ac = slot_a(st, tc), bc = slot_b(st, tc);
-            const int ixx = pk(ar, ac), ixy = pk(ar, bc), ixz = pk(br, ac), ixw = pk(br, bc);
-            const float x = XA[ixx], y = XA[ixy], z = XA[ixz], w = XA[ixw];
-            const float x1 = cc * x - sc * y, y1 = sc * x + cc * y;
-            const float z1 = cc * z - sc * w, w1 = sc * z + cc * w;
-            XB[ixx] = cr * x1 - sr * z1;
-            XB[ixz] = sr * x1 + cr * z1;
-            XB[ixy] = cr * y1 - sr * w1;
-            XB[ixw] = sr * y1 + cr * w1;
-          } else {
-            const int ixx = pk(ar, ar), ixw = pk(br, br), ixy = pk(ar, br);
-            const float x = XA[ixx], y = XA[ixy], w = XA[ixw];
-            const float x1 = cc * x - sc * y, y1 = sc * x + cc * y;
-            const float z1 = cc * y - sc * w, w1 = sc * y + cc * w;
-            XB[ixx] = cr * x1 - sr * z1;
-            XB[ixy] = cr * y1 - sr * w1;
-            XB[ixw] = sr * y1 + cr * w1;
+      __syncthreads();
+      const int step_rot = nrot[ci];
+      if (step_rot != 0) {
+        int tr = tr0, tc = tc0;
+        for (int idx = tid; idx < half * half; idx += NT) {
+          const f32x4 qr = rotp[tr], qc = rotp[tc];
+          const int ar = __float_as_int(qr[2]), br = __float_as_int(qr[3]);
+          const int ac = __float_as_int(qc[2]), bc = __float_as_int(qc[3]);
+          const float cr = qr[0], sr = qr[1], cc = qc[0], sc = qc[1];
+          const float x = X1[ar * p + ac], y = X1[ar * p + bc];
+          const float z = X1[br * p + ac], w = X1[br * p + bc];
+          const float x1 = cc * x - sc * y, y1 = sc * x + cc * y;
+          const float z1 = cc * z - sc * w, w1 = sc * z + cc * w;
+          X1[ar * p + ac] = cr * x1 - sr * z1;
+          X1[br * p + ac] = sr * x1 + cr * z1;
+          X1[ar * p + bc] = cr * y1 - sr * w1;
+          X1[br * p + bc] = sr * y1 + cr * w1;
+          tr += dq;
+          tc += dr;
+          if (tc >= half) {
+            tc -= half;
+            ++tr;
           }
         }
-      }
-      // V: rotate this lane's slots, then move to step st + 1's slots (a-players one
-      // slot down, b-players one slot up; slot 0's a is the fixed player p - 1)
-      {
-        float nA[MS], nB[MS];
-#pragma unroll
-        for (int u = 0; u < MS; ++u) {
-          const int src = ts0 + (u < m ? u : 0);
-          const float c = __shfl(rc, src), sn = __shfl(rs, src);
-          const float a = vA[u], b = vB[u];
-          nA[u] = c * a - sn * b;
-          nB[u] = sn * a + c * b;
-        }
-        // (no register array is indexed by the runtime m: selects over static indices)
-        float lastB = nB[0];
-#pragma unroll
-        for (int u = 1; u < MS; ++u) lastB = (u == m - 1) ? nB[u] : lastB;
-        const float fromUp = __shfl_down(nA[0], 1, 4);  // lane q + 1's nA[0]
-        const float fromDown = __shfl_up(lastB, 1, 4);  // lane q - 1's nB[m - 1]
-        const float tailA = (vq == 3) ? lastB : fromUp;  // slot h - 1: a <- its own b
-#pragma unroll
-        for (int u = 0; u < MS; ++u) {
-          const float na = (u + 1 < MS) ? nA[u + 1 < MS ? u + 1 : u] : 0.f;
-          vA[u] = (u == m - 1) ? tailA : na;
-          if (u >= 1) vB[u] = nB[u - 1];
-        }
-        vB[0] = fromDown;
-        if (vq == 0) {  // slot 0: a is the fixed player, b <- slot 1's a
-          vA[0] = nA[0];
-          vB[0] = nA[1];
+        tr = tr0;
+        tc = tc0;
+        for (int idx = tid; idx < p * half; idx += NT) {
+          const int r = tr, t = tc;
+          tr += dq;
+          tc += dr;
+          if (tc >= half) {
+            tc -= half;
+            ++tr;
+          }
+          const f32x4 qt = rotp[t];
+          const int a = __float_as_int(qt[2]), b = __float_as_int(qt[3]);
+          const float c = qt[0], s = qt[1];
+          const float va = X2[r * p + a], vb = X2[r * p + b];
+          X2[r * p + a] = c * va - s * vb;
+          X2[r * p + b] = s * va + c * vb;
         }
       }
-      float* t = XA;
-      XA = XB;
-      XB = t;
       __syncthreads();
+      if (tid == 0) {
+        nrot[0] += step_rot;
+        nrot[ci] = 0;
+      }
     }
-    if (tid == 0) nrot[0] = swrot_acc;
     __syncthreads();
     const int swrot = nrot[0];
     if (tid == 0) {
@@ -948,22 +900,12 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
   }
 
   stamp(7);
-  // ---- 5. eigenvalues; V (full sweeps: back at step 0's slots) -> X1 = W = D V
-  for (int a = tid; a < p; a += NT) lamv[a] = XA[a * (a + 1) / 2 + a];
-  if (vact) {
-#pragma unroll
-    for (int u = 0; u < MS; ++u) {
-      if (u < m) {
-        const int t = ts0 + u;
-        const int ca = t == 0 ? p - 1 : t, cb = t == 0 ? 0 : p - 1 - t;
-        X1[vr * p + ca] = vA[u] * dsc[vr];
-        X1[vr * p + cb] = vB[u] * dsc[vr];
-      }
-    }
-  }
+  // ---- 5. eigenvalues; W = D (L^-T U) in X2 (row scaling in place); X1 = scratch
+  for (int a = tid; a < p; a += NT) lamv[a] = X1[a * p + a];
   __syncthreads();
-  float* Wm = X1;   // W = D L^-T U
-  float* Ts = X2;   // scratch (ld p)
+  for (int idx = tid; idx < pp; idx += NT) X2[idx] *= dsc[idx / p];
+  float* Wm = X2;   // W = D L^-T U
+  float* Ts = X1;   // scratch (ld p)
   for (int idx = tid; idx < pp; idx += NT) {
     const int a = idx / p, b = idx - a * p;
     Ts[idx] = Gg[a * ldc + b];
@@ -1479,7 +1421,7 @@ size_t rr_small_shm(int p) {
   return (size_t)(2 * p * p + 7 * p + RT / 64 + 20) * sizeof(float);
 }
 
-constexpr int RT2 = 512;  // rr_small2: 4 lanes per row of V for p <= 128
+constexpr int RT2 = 1024;  // rr_small2 (the Jacobi's per-step work wants every thread)
 size_t rr_small2_shm(int p) {
   return (size_t)(2 * p * p + 9 * p + 16 * 17 + 4 + 16 * (p + 4) + RT2 / 64 + 2 + 4) * sizeof(float);
 }
