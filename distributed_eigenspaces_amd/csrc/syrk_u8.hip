@@ -177,7 +177,7 @@ struct U8Sched {
 // no int64 image, no memset, no atomics, no finalize pass (c1 worker shard: the
 // image path's memset + atomics + finalize were most of its 0.30 ms, r03s).
 template <bool DIRECT>
-__global__ __launch_bounds__(SYRK_THR) void u8_syrk_kernel(U8Sched s) {
+__global__ __launch_bounds__(SYRK_THR, 2) void u8_syrk_kernel(U8Sched s) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[2][2][4 * TB * 16];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = tid >> 6, wi = wave >> 1, wj = wave & 1;
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(SYRK_THR) void u8_syrk_kernel(U8Sched s) {
 #pragma unroll
   for (int u = 0; u < PF; ++u)
     if (kb + u < k1) body(kb + u, u);
-  if (!active) return;
+  if (!DIRECT && !active) return;  // (the direct epilogue has barriers: every wave stays)
   // C/D map (gfx950, dtype independent): column = lane & 15, row = 4 (lane >> 4) + reg
   if constexpr (DIRECT) {
     // every column sum loaded up front at clamped indices (a load inside the i < d
@@ -281,29 +281,86 @@ __global__ __launch_bounds__(SYRK_THR) void u8_syrk_kernel(U8Sched s) {
         const int64_t i = i0 + 64 * wi + 16 * a + 4 * (lane >> 4) + r;
         civ[a][r] = (long long)s.colsum[i < s.d ? i : s.d - 1];
       }
+    // values of this wave's 64 x 64 block (float for S; S64 stored here, scattered)
+    float vf[4][4][4];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t i = i0 + 64 * wi + 16 * a + 4 * (lane >> 4) + r;
-        if (i >= s.d) continue;
-        const long long ci = civ[a][r];
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           const int64_t j = j0 + 64 * wj + 16 * b + (lane & 15);
-          if (j >= s.d || (diag && j > i)) continue;
-          const long long v64 = (long long)acc[a][b][r] + 128ll * (ci + cjv[b]) + 16384ll * s.n;
+          const long long v64 =
+              (long long)acc[a][b][r] + 128ll * (civ[a][r] + cjv[b]) + 16384ll * s.n;
           const double v = s.div > 0 ? (double)v64 / (double)s.div : s.alpha * (double)v64;
-          if (s.S) {
-            s.S[i * s.lds + j] = (float)v;
-            s.S[j * s.lds + i] = (float)v;
-          }
-          if (s.S64) {
+          vf[a][b][r] = (float)v;
+          if (s.S64 && active && i < s.d && j < s.d && !(diag && j > i)) {
             s.S64[i * s.lds64 + j] = v;
             s.S64[j * s.lds64 + i] = v;
           }
         }
       }
+    if (s.S) {
+      // S[i][j]: 16 consecutive j per row and instruction
+      if (active)
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int64_t i = i0 + 64 * wi + 16 * a + 4 * (lane >> 4) + r;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+              const int64_t j = j0 + 64 * wj + 16 * b + (lane & 15);
+              if (i < s.d && j < s.d && !(diag && j > i)) s.S[i * s.lds + j] = vf[a][b][r];
+            }
+          }
+      // the mirror S[j][i] through LDS, one 64-row half of the tile at a time: the
+      // stage buffers (32 KiB, free after the K loop's last barrier) hold the half as
+      // 64 x 128 floats, columns XOR-swizzled by the row; then 16 threads per S row
+      // write 64 contiguous floats (float4 each).  (Stored straight from the
+      // accumulators, every mirror instruction scattered 4-byte writes over 64 rows:
+      // r04 A/B in one process on the c1 worker shard, 99.7 vs 102.5 us per covariance,
+      // bit-identical, profiles/r04b_u8_mirror_ab.log.)
+      float* T = reinterpret_cast<float*>(&lds[0][0][0]);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (active && wi == h)
+#pragma unroll
+          for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int il = 16 * a + 4 * (lane >> 4) + r;
+#pragma unroll
+              for (int b = 0; b < 4; ++b) {
+                const int jl = 64 * wj + 16 * b + (lane & 15);
+                T[il * 128 + (jl ^ (il & 31))] = vf[a][b][r];
+              }
+            }
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+          const int task = it * SYRK_THR + tid;  // (S row j0 + jl, rows i4 .. i4 + 3 of the half)
+          const int jl = task >> 4, i4 = (task & 15) * 4;
+          const int64_t j = j0 + jl;
+          const int64_t ib = i0 + 64 * h + i4;
+          if (j < s.d) {
+            float x[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[e] = T[(i4 + e) * 128 + (jl ^ ((i4 + e) & 31))];
+            float* dst = s.S + j * s.lds + ib;
+            if (!diag && ib + 3 < s.d && (reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+              *reinterpret_cast<f32x4*>(dst) = f32x4{x[0], x[1], x[2], x[3]};
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                if (ib + e < s.d && (!diag || j < ib + e)) dst[e] = x[e];
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
     return;
   }
   unsigned long long* Gp = s.G + (int64_t)plane * s.fpad * s.fpad;
