@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 OUT=gpurun_out/r04d
 mkdir -p $OUT
-timeout -k 10 500 python -u tools/rr_phases_ab.py tools/ab_libs/libdeig_rrv1.so > $OUT/rr_phases.log 2>&1 || { tail -30 $OUT/rr_phases.log; exit 1; }
+timeout -k 10 500 python -u tools/rr_phases_ab.py tools/ab_libs/libdeig_rrv1.so tools/ab_libs/libdeig_rrjlow.so > $OUT/rr_phases.log 2>&1 || { tail -30 $OUT/rr_phases.log; exit 1; }
 cat $OUT/rr_phases.log
 timeout -k 10 500 python -u -m pytest -v --timeout 200 --timeout-method thread \
   tests/test_gpu_syrk_chunks.py tests/test_gpu_integration_stub.py \

@@ -24,21 +24,25 @@ LIBDIR = os.path.join(ROOT, "tools", "ab_libs")
 V1 = os.path.join(LIBDIR, "libdeig_rrv1.so")
 
 
+JLOW = os.path.join(LIBDIR, "libdeig_rrjlow.so")
+
+
 def build():
     from distributed_eigenspaces_amd import _build
     os.makedirs(LIBDIR, exist_ok=True)
     _build.build_library()
     objdir = os.path.join(_build.HERE, "build")
     hipcc = _build._hipcc()
-    obj = os.path.join(LIBDIR, "rr_v1.o")
-    subprocess.run([hipcc, f"--offload-arch={_build.ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-                    "-Wno-unused-function", "-Wno-inline-asm", "-DDEIG_AB_RR_V1", "-c",
-                    os.path.join(_build.CSRC, "rr.hip"), "-o", obj], check=True)
     others = [os.path.join(objdir, s.replace(".hip", ".o")) for s in _build.SOURCES if s != "rr.hip"]
-    subprocess.run([hipcc, f"--offload-arch={_build.ARCH}", "-shared", "-fPIC", "-o", V1, obj] + others,
-                   check=True)
-    os.remove(obj)
-    print("built", V1)
+    for define, out in (("-DDEIG_AB_RR_V1", V1), ("-DDEIG_AB_RR_JLOW", JLOW)):
+        obj = out + ".o"
+        subprocess.run([hipcc, f"--offload-arch={_build.ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+                        "-Wno-unused-function", "-Wno-inline-asm", define, "-c",
+                        os.path.join(_build.CSRC, "rr.hip"), "-o", obj], check=True)
+        subprocess.run([hipcc, f"--offload-arch={_build.ARCH}", "-shared", "-fPIC", "-o", out, obj] + others,
+                       check=True)
+        os.remove(obj)
+        print("built", out)
 
 
 def _bind(path):
