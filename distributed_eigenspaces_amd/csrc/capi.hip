@@ -12,9 +12,8 @@
 
 #include <algorithm>
 #include <atomic>
-#include <condition_variable>
 #include <mutex>
-#include <thread>
+#include <tuple>
 #include <vector>
 
 #include "deig_internal.hpp"
@@ -328,11 +327,19 @@ struct HostStatus {
   int jconv;
 };
 
+// blockIdx.x: the problem of a batched launch (buffers at pbt.off, status block pbt.hs).
 __global__ __launch_bounds__(256) void status_kernel(const float* __restrict__ resid, int nres,
                                                      const float* __restrict__ lam, int pb,
                                                      const int* __restrict__ info,
-                                                     HostStatus* __restrict__ hs) {
-  const int t = threadIdx.x;
+                                                     const ProbBatch pbt) {
+  const int t = threadIdx.x, prob = blockIdx.x;
+  HostStatus* __restrict__ hs = static_cast<HostStatus*>(pbt.hs[prob]);
+  if (prob) {
+    const int64_t o = pbt.off[prob];
+    resid = reinterpret_cast<const float*>(reinterpret_cast<const char*>(resid) + o);
+    lam = reinterpret_cast<const float*>(reinterpret_cast<const char*>(lam) + o);
+    info = reinterpret_cast<const int*>(reinterpret_cast<const char*>(info) + o);
+  }
   if (t < nres) hs->res[t] = resid[t];
   if (t < pb) hs->lam[t] = lam[t];
   if (t == 0) hs->jconv = info[3];
@@ -454,11 +461,37 @@ struct Solver {
     converged = false;
   }
 
+  // The cycle's sweeps, planned on the host (plan_cycle) and then enqueued (run_plan,
+  // or solve_batch's batched launches across problems).
+  struct PlanItem {
+    SweepStep step;
+    bool has_step;  // a fused basis step follows the product
+    int smode;
+    bool q_ready;   // this sweep's Q image was written by the previous one
+  };
+  std::vector<PlanItem> plan;
+
   // Enqueue the cycle's sweeps and the Gram; *ended: the sweep budget is spent (the
   // iteration is over, nothing was enqueued).
   int cycle_sweeps(bool* ended) {
-    *ended = !(it - start < max_sweeps);
+    plan_cycle(ended);
     if (*ended) return DEIG_OK;
+    int rc;
+    for (const PlanItem& pi : plan)
+      if ((rc = apply_op(op, w, d, pb, st, pi.smode, pi.has_step ? &pi.step : nullptr, pi.q_ready)))
+        return rc;
+    return gram(st);
+  }
+
+  int gram(hipStream_t s) {
+    return skinny_launch(true, w.rr.Z, 2 * pb, w.rr.Z, 2 * pb, w.rr.C, 2 * pb, 2 * pb, 2 * pb, d, 1.f,
+                         0.f, w.slab, w.slab_bytes, s);
+  }
+
+  void plan_cycle(bool* ended) {
+    plan.clear();
+    *ended = !(it - start < max_sweeps);
+    if (*ended) return;
     const int budget = max_sweeps - (it - start);
     // Sweep precision by residual: early sweeps (above fast_until) take S as its
     // two leading bf16 pieces too - three products, no split in the sweep, ~2^-16
@@ -469,9 +502,9 @@ struct Solver {
     const int smode = (o.fast_until > 0.f && last > fmaxf(o.fast_until, tol)) ? kSweepFast
                       : last > fmaxf(o.round_until, tol)                      ? kSweepRoundQ
                                                                               : kSweepExact;
-    ChebPlan plan;
-    const bool cheb = o.cheb && nrr > 0 && cheb_plan(lam_h, kc, pb, last, tol, o.cheb_above, &plan);
-    int nstep = 0, rc;
+    ChebPlan cp;
+    const bool cheb = o.cheb && nrr > 0 && cheb_plan(lam_h, kc, pb, last, tol, o.cheb_above, &cp);
+    int nstep = 0;
     ncheb_dbg = 0;
     SweepStep step{};
     step.Q = w.rr.Z;
@@ -482,25 +515,25 @@ struct Solver {
     step.next_mode = smode;
     if (cheb) {
       // degree j: apply A to X_j, then X_{j+1} from X_j, A X_j and X_{j-1}
-      const int m = std::min(plan.m, budget - 1);
-      double s_prev = plan.s1;
+      const int m = std::min(cp.m, budget - 1);
+      double s_prev = cp.s1;
       for (int j = 0; j < m; ++j, ++it, ++nstep) {
         double alpha, gamma;
         if (j == 0) {
-          alpha = plan.s1 / plan.e;
+          alpha = cp.s1 / cp.e;
           gamma = 0.0;
         } else {
-          const double s_next = 1.0 / (2.0 / plan.s1 - s_prev);
-          alpha = 2.0 * s_next / plan.e;
+          const double s_next = 1.0 / (2.0 / cp.s1 - s_prev);
+          alpha = 2.0 * s_next / cp.e;
           gamma = s_prev * s_next;
           s_prev = s_next;
         }
         step.kind = 2;
-        step.thr = plan.thr;
+        step.thr = cp.thr;
         step.a = (float)alpha;
-        step.cc = (float)plan.cc;
+        step.cc = (float)cp.cc;
         step.gamma = (float)gamma;
-        if ((rc = apply_op(op, w, d, pb, st, smode, &step, fuse && nstep > 0))) return rc;
+        plan.push_back({step, true, smode, fuse && nstep > 0});
       }
       ncheb_dbg = m;
     } else if (nrr > 0) {
@@ -508,17 +541,14 @@ struct Solver {
       // power steps on the live Ritz columns of the last RR (Q_j <- Y_j / ||Y w_j||)
       step.kind = 1;
       step.tau = tau;
-      for (int j = 0; j < npow; ++j, ++it, ++nstep)
-        if ((rc = apply_op(op, w, d, pb, st, smode, &step, fuse && nstep > 0))) return rc;
+      for (int j = 0; j < npow; ++j, ++it, ++nstep) plan.push_back({step, true, smode, fuse && nstep > 0});
     }
-    if ((rc = apply_op(op, w, d, pb, st, smode, nullptr, fuse && nstep > 0))) return rc;
+    plan.push_back({step, false, smode, fuse && nstep > 0});
     ++it;
     // The next basis Y W spans span(Y) for any invertible W, so subspace progress
     // does not need converged Ritz vectors; the residual of approximate pairs only
     // over-states the error (no false convergence).
     jcap = (jcap_sweeps > 0 && last > jcap_above) ? jcap_sweeps : 30;
-    return skinny_launch(true, w.rr.Z, 2 * pb, w.rr.Z, 2 * pb, w.rr.C, 2 * pb, 2 * pb, 2 * pb, d, 1.f,
-                         0.f, w.slab, w.slab_bytes, st);
   }
 
   int cycle_rr_small() { return rr_small_launch(w.rr, pb, st, jcap); }
@@ -527,8 +557,10 @@ struct Solver {
   int cycle_update() {
     int rc;
     if ((rc = rr_update_launch(w.rr, d, pb, kc, Vb, ldv, evb, st))) return rc;
+    ProbBatch one = one_problem();
+    one.hs[0] = hs;
     hipLaunchKernelGGL(status_kernel, dim3(1), dim3(256), 0, st, w.rr.resid, kc + 1, w.rr.lam, pb,
-                       w.rr.info, hs);
+                       w.rr.info, one);
     DEIG_HIP_CHECK(hipGetLastError());
     return DEIG_OK;
   }
@@ -1018,147 +1050,205 @@ int solve(const Operator& op0, int64_t d, int k, int p, int max_sweeps, float to
   return sm.outcome(sweeps_out, resid_out);
 }
 
-// W independent explicit-S problems (same d, k, p) advanced in lockstep.  One host
-// thread per problem enqueues that problem's sweeps, Gram and updates on its own
-// stream (one thread issuing every problem's launches was host-bound: ~15 launches
-// per problem and round, r03l); at each Rayleigh-Ritz step the threads meet at a
-// barrier and the last one to arrive launches the small solves of all arrived
-// problems in ONE launch (one workgroup each, on `st`, after every participant's
-// Gram), which each then waits for on its own stream.  A problem that is between
-// blocks joins the next round; one that is done leaves the barrier.  Results are
-// those of W separate solve() calls (same kernels, same decisions, tested bit for
-// bit); what changes is that W single-workgroup solves share a launch instead of W
-// streams contending for the hardware queues.
+// Two solvers whose workspaces are carved alike (every buffer at the same offset
+// *off from A's): one batched launch can cover both.
+bool same_layout(const SolverWs& a, const SolverWs& b, int64_t* off) {
+  auto dl = [](const void* y, const void* x) {
+    return (int64_t)(reinterpret_cast<uintptr_t>(y) - reinterpret_cast<uintptr_t>(x));
+  };
+  const int64_t o = dl(b.rr.Z, a.rr.Z);
+  *off = o;
+  const void* pa[] = {a.rr.C, a.rr.Linv, a.rr.Wtmp, a.rr.W, a.rr.lam, a.rr.cs, a.rr.qs,
+                      a.rr.resid_part, a.rr.resid, a.rr.info, a.Zt, a.T, a.Tdef, a.rq, a.slab,
+                      a.sweep_ws};
+  const void* pb[] = {b.rr.C, b.rr.Linv, b.rr.Wtmp, b.rr.W, b.rr.lam, b.rr.cs, b.rr.qs,
+                      b.rr.resid_part, b.rr.resid, b.rr.info, b.Zt, b.T, b.Tdef, b.rq, b.slab,
+                      b.sweep_ws};
+  for (size_t i = 0; i < sizeof(pa) / sizeof(pa[0]); ++i) {
+    if (!pa[i] != !pb[i]) return false;
+    if (pa[i] && dl(pb[i], pa[i]) != o) return false;
+  }
+  return a.slab_bytes == b.slab_bytes && a.sweep_bytes == b.sweep_bytes;
+}
+
+// W independent explicit-S problems (same d, k, p) advanced in lockstep by one host
+// thread on one stream.  Each round: every problem is brought to its next cycle
+// (block set-up, locking, restarts: its own launches) and plans that cycle's sweeps
+// (Solver::plan_cycle); then the cycle of all of them is enqueued as batched launches
+// - the j-th sweep of every plan in one launch per kernel (sweep.hip SweepBatch: c1's
+// 8 problems at d = 3072 each filled only 144 CUs), one Gram launch, the small
+// solves in one launch (one workgroup each), one update and one status launch - and
+// ONE stream sync precedes every problem's host decision (cycle_finish).  Problems
+// are grouped per launch by shape and mode (a block of k > 128 pairs may be
+// narrower, a plan shorter); a problem that is done drops out.  r03 ran one host
+// thread and stream per problem and met only at the small solves: 8 x 29 sweeps of
+// 144 blocks contending for the queues, ~15 small launches per problem and round,
+// and a barrier, a sync and a thread wake-up per problem and round (profiles/r04e).
+// Results are those of W separate solve() calls (same kernels, split-K slicing and
+// decisions; tested bit for bit).
 int solve_batch(int W, const Operator* ops, int64_t d, int k, int p, int max_sweeps, float tol,
                 float* const* V, int64_t ldv, float* const* evals, int* sweeps_out, float* resid_out,
-                int* status_out, const Opts& o, char* ws, size_t ws_each, const hipStream_t* streams,
-                hipStream_t st) {
+                int* status_out, const Opts& o, char* ws, size_t ws_each, hipStream_t st) {
   DEIG_REQUIRE(W >= 1 && W <= 1024, "solve_batch: W=%d out of range", W);
-  int dev = 0;
-  DEIG_HIP_CHECK(hipGetDevice(&dev));
   std::vector<SolveSM> sm(W);
-  std::vector<hipEvent_t> ev(W + 1, nullptr);
   int rc = DEIG_OK;
-  for (int i = 0; i <= W && !rc; ++i)
-    if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess)
-      rc = fail(DEIG_EHIP, "solve_batch: event creation failed");
   for (int i = 0; i < W && !rc; ++i)
     rc = sm[i].init(ops[i], d, k, p, max_sweeps, tol, nullptr, 0, 0, V[i], ldv, evals[i], o,
-                    ws + (size_t)i * ws_each, ws_each, streams[i]);
-  if (rc) {
-    for (hipEvent_t e : ev)
-      if (e) (void)hipEventDestroy(e);
-    return rc;
-  }
-  struct Coord {
-    std::mutex mu;
-    std::condition_variable cv;
-    int active = 0;          // problems not finished
-    std::vector<int> here;   // problems waiting at the barrier of this generation
-    long gen = 0;
-    int err = DEIG_OK;
-    char msg[1024] = "";
-  } co;
-  co.active = W;
-  std::vector<int> jc;
+                    ws + (size_t)i * ws_each, ws_each, st);
+  if (rc) return rc;
+  std::vector<int> cyc, grp;
+  std::vector<char> taken;
+  // Launch groups: up to kMaxProbBatch problems of `mem` that agree on key and are
+  // laid out alike; f(grp, batch) enqueues one group.
+  auto groups = [&](const std::vector<int>& mem, auto key, auto f) {
+    taken.assign(mem.size(), 0);
+    for (size_t a = 0; a < mem.size(); ++a) {
+      if (taken[a]) continue;
+      ProbBatch b = one_problem();
+      grp.assign(1, mem[a]);
+      taken[a] = 1;
+      const auto ka = key(mem[a]);
+      for (size_t c = a + 1; c < mem.size() && b.n < kMaxProbBatch; ++c) {
+        int64_t off = 0;
+        if (taken[c] || !(key(mem[c]) == ka) || !same_layout(sm[mem[a]].sv.w, sm[mem[c]].sv.w, &off))
+          continue;
+        taken[c] = 1;
+        b.off[b.n++] = off;
+        grp.push_back(mem[c]);
+      }
+      if (int r = f(grp, b)) return r;
+    }
+    return (int)DEIG_OK;
+  };
+  std::vector<int> at_j;
   std::vector<const RRBuffers*> bufs;
-  // with co.mu held: the small solves of every waiting problem, then release them
-  auto launch_round = [&]() {
-    int r = DEIG_OK;
-    for (int i : co.here)
-      if (hipStreamWaitEvent(st, ev[i], 0) != hipSuccess)
-        r = fail(DEIG_EHIP, "solve_batch: stream wait failed");
-    // one launch per subspace width (the last block of k > 128 pairs may be narrower)
-    for (size_t a = 0; a < co.here.size() && !r; ++a) {
-      const int pw = sm[co.here[a]].sv.pb;
+  std::vector<int> jc;
+  // one round's cycles (stream-ordered after every problem's set-up launches)
+  auto run_round = [&]() -> int {
+    size_t L = 0;
+    for (int i : cyc) L = std::max(L, sm[i].sv.plan.size());
+    int r;
+    for (size_t j = 0; j < L; ++j) {  // sweeps: the j-th of every plan
+      at_j.clear();
+      for (int i : cyc)
+        if (j < sm[i].sv.plan.size()) at_j.push_back(i);
+      r = groups(
+          at_j,
+          [&](int i) {
+            const Solver& s = sm[i].sv;
+            const Solver::PlanItem& x = s.plan[j];
+            return std::make_tuple(s.pb, x.smode, x.has_step, x.q_ready, x.step.next_mode,
+                                   s.w.sweep_ws != nullptr);
+          },
+          [&](const std::vector<int>& g, ProbBatch& b) {
+            const Solver& A = sm[g[0]].sv;
+            const Solver::PlanItem& x = A.plan[j];
+            if (b.n == 1 || !A.w.sweep_ws)
+              return apply_op(A.op, A.w, A.d, A.pb, st, x.smode, x.has_step ? &x.step : nullptr, x.q_ready);
+            SweepBatch sb{};
+            sb.n = b.n;
+            for (int m = 0; m < b.n; ++m) {
+              const SweepStep& y = sm[g[m]].sv.plan[j].step;
+              sb.off[m] = b.off[m];
+              sb.kind[m] = y.kind;
+              sb.tau[m] = y.tau;
+              sb.thr[m] = y.thr;
+              sb.a[m] = y.a;
+              sb.cc[m] = y.cc;
+              sb.gamma[m] = y.gamma;
+            }
+            const int64_t ld = 2 * A.pb;
+            return sweep_apply(A.w.rr.Z, A.d, A.pb, ld, A.w.rr.Z + A.pb, ld, 1.f, A.w.sweep_ws,
+                               A.w.sweep_bytes, st, x.smode, x.has_step ? &x.step : nullptr, x.q_ready,
+                               false, &sb);
+          });
+      if (r) return r;
+    }
+    // Grams
+    r = groups(cyc, [&](int i) { return sm[i].sv.pb; },
+               [&](const std::vector<int>& g, ProbBatch& b) {
+                 const Solver& A = sm[g[0]].sv;
+                 const int n2 = 2 * A.pb;
+                 return skinny_launch(true, A.w.rr.Z, n2, A.w.rr.Z, n2, A.w.rr.C, n2, n2, n2, A.d, 1.f,
+                                      0.f, A.w.slab, A.w.slab_bytes, st, &b);
+               });
+    if (r) return r;
+    // small solves: one launch per subspace width (the last block of k > 128 pairs may
+    // be narrower)
+    for (size_t a = 0; a < cyc.size(); ++a) {
+      const int pw = sm[cyc[a]].sv.pb;
       bool seen = false;
-      for (size_t b = 0; b < a; ++b) seen |= sm[co.here[b]].sv.pb == pw;
+      for (size_t c = 0; c < a; ++c) seen |= sm[cyc[c]].sv.pb == pw;
       if (seen) continue;
       bufs.clear();
       jc.clear();
-      for (int i : co.here)
+      for (int i : cyc)
         if (sm[i].sv.pb == pw) {
           bufs.push_back(&sm[i].sv.w.rr);
           jc.push_back(sm[i].sv.jcap);
         }
-      r = rr_small_batch_launch(bufs.data(), jc.data(), (int)bufs.size(), pw, st);
+      if ((r = rr_small_batch_launch(bufs.data(), jc.data(), (int)bufs.size(), pw, st))) return r;
     }
-    if (!r && hipEventRecord(ev[W], st) != hipSuccess) r = fail(DEIG_EHIP, "solve_batch: event record failed");
-    if (r && !co.err) {
-      co.err = r;
-      snprintf(co.msg, sizeof(co.msg), "%s", g_err);
-    }
-    co.here.clear();
-    ++co.gen;
-    co.cv.notify_all();
+    // Ritz vectors, residuals and the status blocks
+    return groups(
+        cyc, [&](int i) { return std::make_tuple(sm[i].sv.pb, sm[i].sv.kc, sm[i].sv.ldv); },
+        [&](const std::vector<int>& g, ProbBatch& b) {
+          const Solver& A = sm[g[0]].sv;
+          for (int m = 0; m < b.n; ++m) {
+            b.V[m] = sm[g[m]].sv.Vb;
+            b.evals[m] = sm[g[m]].sv.evb;
+            b.hs[m] = sm[g[m]].sv.hs;
+          }
+          int r2 = rr_update_batch_launch(A.w.rr, A.d, A.pb, A.kc, A.ldv, b, st);
+          if (r2) return r2;
+          hipLaunchKernelGGL(status_kernel, dim3((unsigned)b.n), dim3(256), 0, st, A.w.rr.resid, A.kc + 1,
+                             A.w.rr.lam, A.pb, A.w.rr.info, b);
+          DEIG_HIP_CHECK(hipGetLastError());
+          return (int)DEIG_OK;
+        });
   };
-  auto run = [&](int i) {
-    (void)hipSetDevice(dev);  // HIP's current device is per thread
-    SolveSM& m = sm[i];
-    int r = DEIG_OK;
-    while (!r) {
-      if ((r = m.settle()) || m.state == SolveSM::DONE) break;
-      bool ended = false, done = false;
-      if ((r = m.sv.cycle_sweeps(&ended))) break;
-      if (ended) {
-        r = m.end_block();
-        continue;
+  while (!rc) {
+    // every problem to its next cycle (or DONE)
+    cyc.clear();
+    for (int i = 0; i < W && !rc; ++i) {
+      SolveSM& m = sm[i];
+      while (m.state != SolveSM::DONE) {
+        if ((rc = m.settle()) || m.state == SolveSM::DONE) break;
+        bool ended = false;
+        m.sv.plan_cycle(&ended);
+        if (!ended) {
+          cyc.push_back(i);
+          break;
+        }
+        if ((rc = m.end_block())) break;
       }
-      if (hipEventRecord(ev[i], streams[i]) != hipSuccess) {
-        r = fail(DEIG_EHIP, "solve_batch: event record failed");
-        break;
-      }
-      {
-        std::unique_lock<std::mutex> lk(co.mu);
-        if (co.err) break;
-        co.here.push_back(i);
-        const long g = co.gen;
-        if ((int)co.here.size() == co.active)
-          launch_round();
-        else
-          co.cv.wait(lk, [&] { return co.gen != g || co.err != DEIG_OK; });
-        if (co.err) break;
-      }
-      if (hipStreamWaitEvent(streams[i], ev[W], 0) != hipSuccess) {
-        r = fail(DEIG_EHIP, "solve_batch: stream wait failed");
-        break;
-      }
-      if ((r = m.sv.cycle_update())) break;
-      if (hipStreamSynchronize(streams[i]) != hipSuccess) {
-        r = fail(DEIG_EHIP, "solve_batch: stream synchronisation failed");
-        break;
-      }
-      if ((r = m.sv.cycle_finish(&done))) break;
-      if (done) r = m.end_block();
+      if (rc) m.rc = rc;
     }
-    std::lock_guard<std::mutex> lk(co.mu);
-    m.rc = r;
-    --co.active;
-    if (r && !co.err) {
-      co.err = r;
-      snprintf(co.msg, sizeof(co.msg), "%s", g_err);
+    if (rc || cyc.empty()) break;
+    if ((rc = run_round())) break;
+    if (hipStreamSynchronize(st) != hipSuccess) {
+      rc = fail(DEIG_EHIP, "solve_batch: stream synchronisation failed");
+      break;
     }
-    if (!co.err && !co.here.empty() && (int)co.here.size() == co.active) launch_round();
-    co.cv.notify_all();
-  };
-  std::vector<std::thread> th;
-  th.reserve(W - 1);
-  for (int i = 1; i < W; ++i) th.emplace_back(run, i);
-  run(0);
-  for (std::thread& t : th) t.join();
-  // every problem's last kernels (eigenvalues) are on its stream: join them into st
-  for (int i = 0; i < W; ++i)
-    if (hipEventRecord(ev[i], streams[i]) == hipSuccess) (void)hipStreamWaitEvent(st, ev[i], 0);
-  for (hipEvent_t e : ev)
-    if (e) (void)hipEventDestroy(e);
-  if (co.err) {
-    set_error("%s", co.msg);
+    for (int i : cyc) {
+      bool done = false;
+      if (!(rc = sm[i].sv.cycle_finish(&done)) && done) rc = sm[i].end_block();
+      if (rc) {
+        sm[i].rc = rc;
+        break;
+      }
+    }
+  }
+  if (rc) {
+    char msg[1024];
+    snprintf(msg, sizeof(msg), "%s", g_err);
     for (int i = 0; i < W; ++i) {
       if (sweeps_out) sweeps_out[i] = sm[i].sv.it;
       if (resid_out) resid_out[i] = sm[i].sv.last;
-      if (status_out) status_out[i] = sm[i].rc ? sm[i].rc : co.err;
+      if (status_out) status_out[i] = sm[i].rc ? sm[i].rc : rc;
     }
-    return co.err;
+    set_error("%s", msg);
+    return rc;
   }
   int first = DEIG_OK;
   char msg[1024] = "";
@@ -1358,19 +1448,17 @@ int deig_topk_sym_batch(int W, const void* const* S, int stype, int64_t d, int64
   if (!ws || ws_bytes < (size_t)W * each)
     return fail(DEIG_EWORKSPACE, "topk_batch: workspace %zu bytes < required %zu", ws_bytes,
                 (size_t)W * each);
+  (void)streams;  // r03's per-problem streams: every launch is on `stream` since r04
   std::vector<Operator> ops(W);
-  std::vector<hipStream_t> sts(W);
   for (int i = 0; i < W; ++i) {
     ops[i] = Operator{};
     ops[i].implicit = false;
     ops[i].S = S[i];
     ops[i].stype = stype;
     ops[i].lds = lds;
-    sts[i] = streams && streams[i] ? (hipStream_t)streams[i] : (hipStream_t)stream;
   }
   return solve_batch(W, ops.data(), d, k, p, max_sweeps, tol, V, ldv, evals, sweeps_out, resid_out,
-                     status_out, make_opts(opts), static_cast<char*>(ws), each, sts.data(),
-                     (hipStream_t)stream);
+                     status_out, make_opts(opts), static_cast<char*>(ws), each, (hipStream_t)stream);
 }
 
 size_t deig_projavg_workspace_ex(int64_t d, int64_t mk, int k, int p,

@@ -92,10 +92,31 @@ int syrk_u8_launch(const uint8_t* X, int64_t n, int64_t d, int64_t ldx, int mode
 //   trans_a = true : A is K x M row-major (op(A) = A^T)
 //   trans_a = false: A is M x K row-major
 //   B is K x N row-major; N % 16 == 0, N <= 256.
+// Launches that cover several problems of one shape (solve_batch): problem i's
+// workspace buffers sit off[i] bytes after problem 0's (off[0] = 0; the solver
+// workspaces are equally carved slices of one allocation); outputs outside the
+// workspaces are per problem.
+constexpr int kMaxProbBatch = 16;
+struct ProbBatch {
+  int n;
+  int64_t off[kMaxProbBatch];
+  float* V[kMaxProbBatch];      // rr_update: the block's eigenvectors
+  float* evals[kMaxProbBatch];  // rr_update: its eigenvalues
+  void* hs[kMaxProbBatch];      // solver status blocks (pinned host memory)
+};
+inline ProbBatch one_problem() {
+  ProbBatch b{};
+  b.n = 1;
+  return b;
+}
+
 size_t skinny_workspace_bytes(int64_t M, int64_t N, int64_t K);
+// batch (optional): the same product for batch->n problems, A, B, C and slab of
+// problem i at off[i] bytes from the arguments.
 int skinny_launch(bool trans_a, const float* A, int64_t lda, const float* B, int64_t ldb,
                   float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha,
-                  float beta, float* slab, size_t slab_bytes, hipStream_t stream);
+                  float beta, float* slab, size_t slab_bytes, hipStream_t stream,
+                  const ProbBatch* batch = nullptr);
 
 // bf16x6 symmetric sweep (sweep.hip): Y = alpha * S Q, S symmetric d x d
 // row-major, Q d x p (ldq), Y d x p (ldy), p % 16 == 0, p <= 128.
@@ -130,10 +151,23 @@ struct SweepStep {
   float thr, a, cc, gamma;  // Chebyshev: X_{j+1} = a (Y - cc X_j) - gamma X_{j-1} if lam_j >= thr
   int next_mode;            // kSweep* of the next sweep
 };
+// Several problems of the same d, p and mode in one launch per kernel (solve_batch):
+// problem i's Q, Y, workspace and step buffers sit off[i] bytes after problem 0's
+// (off[0] = 0); the fused step's scalars are per problem, its pointers and next_mode
+// problem 0's.
+constexpr int kMaxSweepBatch = kMaxProbBatch;
+struct SweepBatch {
+  int n;
+  int64_t off[kMaxSweepBatch];
+  int kind[kMaxSweepBatch];
+  float tau[kMaxSweepBatch], thr[kMaxSweepBatch], a[kMaxSweepBatch], cc[kMaxSweepBatch],
+      gamma[kMaxSweepBatch];
+};
 int sweep_apply(const float* Q, int64_t d, int p, int64_t ldq, float* Y, int64_t ldy, float alpha,
                 void* ws, size_t ws_bytes, hipStream_t st, int mode = kSweepExact,
                 const SweepStep* step = nullptr, bool q_ready = false,
-                bool kernel_only = false);  // kernel_only: no split-K reduction (measurement)
+                bool kernel_only = false,  // kernel_only: no split-K reduction (measurement)
+                const SweepBatch* batch = nullptr);
 
 // Rayleigh-Ritz pieces (rr.hip).
 struct RRBuffers {
@@ -167,6 +201,9 @@ int cheb_step_launch(const RRBuffers& b, float* T, int64_t d, int p, float thr, 
                      float cc, float gamma, hipStream_t stream);
 int rr_update_launch(const RRBuffers& b, int64_t d, int p, int k, float* V, int64_t ldv,
                      float* evals, hipStream_t stream);
+// The same for batch.n problems (RRBuffers of problem i at off[i]; V / evals per problem).
+int rr_update_batch_launch(const RRBuffers& b0, int64_t d, int p, int k, int64_t ldv,
+                           const ProbBatch& batch, hipStream_t stream);
 // Columns 0..kc-1 of V (col-major, ldv) made orthogonal to columns kc..kc+r-1, normalised.
 int deflate_orth_launch(float* V, int64_t ldv, int64_t d, int kc, int r, hipStream_t stream);
 // Columns 0..kc-1 of V orthonormalised among themselves in order (modified Gram-Schmidt,

@@ -1072,14 +1072,26 @@ __global__ __launch_bounds__(NT) void rr_small2_batch_kernel(RRBatchArgs a, int 
   rr_small2_body<NT>(a.C[i], p, a.W[i], a.lam[i], a.cs[i], a.qs[i], a.info[i], a.max_jsweeps[i], jrel);
 }
 
+// blockIdx.y: the problem of a batched launch (its buffers at pbt.off, V = pbt.V).
 __global__ __launch_bounds__(256) void rr_update_kernel(float* __restrict__ Z, int64_t d, int p,
                                                         int k, const float* __restrict__ W,
                                                         const float* __restrict__ lam,
                                                         const float* __restrict__ cs,
-                                                        const float* __restrict__ qs,
-                                                        float* __restrict__ V, int64_t ldv,
-                                                        float* __restrict__ resid_part) {
+                                                        const float* __restrict__ qs, int64_t ldv,
+                                                        float* __restrict__ resid_part,
+                                                        const ProbBatch pbt) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int prob = blockIdx.y;
+  float* __restrict__ V = pbt.V[prob];
+  if (prob) {
+    const int64_t o = pbt.off[prob];
+    Z = reinterpret_cast<float*>(reinterpret_cast<char*>(Z) + o);
+    W = reinterpret_cast<const float*>(reinterpret_cast<const char*>(W) + o);
+    lam = reinterpret_cast<const float*>(reinterpret_cast<const char*>(lam) + o);
+    cs = reinterpret_cast<const float*>(reinterpret_cast<const char*>(cs) + o);
+    qs = reinterpret_cast<const float*>(reinterpret_cast<const char*>(qs) + o);
+    resid_part = reinterpret_cast<float*>(reinterpret_cast<char*>(resid_part) + o);
+  }
   float* Ws = sm;                  // p x p
   float* Zs = sm + p * p;          // UR x 2p
   float* rp = Zs + UR * 2 * p;     // ngrp x k partial residuals
@@ -1133,9 +1145,17 @@ __global__ __launch_bounds__(256) void rr_update_kernel(float* __restrict__ Z, i
 __global__ __launch_bounds__(256) void rr_finish_kernel(const float* __restrict__ resid_part,
                                                         int nblk, int k,
                                                         const float* __restrict__ lam,
-                                                        float* __restrict__ evals,
-                                                        float* __restrict__ resid) {
+                                                        float* __restrict__ resid,
+                                                        const ProbBatch pbt) {
   __shared__ float mx[4];
+  const int prob = blockIdx.x;
+  float* __restrict__ evals = pbt.evals[prob];
+  if (prob) {
+    const int64_t o = pbt.off[prob];
+    resid_part = reinterpret_cast<const float*>(reinterpret_cast<const char*>(resid_part) + o);
+    lam = reinterpret_cast<const float*>(reinterpret_cast<const char*>(lam) + o);
+    resid = reinterpret_cast<float*>(reinterpret_cast<char*>(resid) + o);
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float scale = fmaxf(fabsf(lam[0]), 1e-30f);
   float m = 0.f;
@@ -1622,18 +1642,27 @@ int rr_update_blocks(int64_t d) { return (int)cdiv(d, UR); }
 
 int rr_update_launch(const RRBuffers& b, int64_t d, int p, int k, float* V, int64_t ldv,
                      float* evals, hipStream_t stream) {
+  ProbBatch one = one_problem();
+  one.V[0] = V;
+  one.evals[0] = evals;
+  return rr_update_batch_launch(b, d, p, k, ldv, one, stream);
+}
+
+int rr_update_batch_launch(const RRBuffers& b, int64_t d, int p, int k, int64_t ldv,
+                           const ProbBatch& pbt, hipStream_t stream) {
   const int nblk = rr_update_blocks(d);
   DEIG_REQUIRE(p >= 16 && p <= 128, "rr_update: p=%d out of range", p);
+  DEIG_REQUIRE(pbt.n >= 1 && pbt.n <= kMaxProbBatch && pbt.off[0] == 0, "rr_update: batch of %d", pbt.n);
   const size_t shm = (size_t)(p * p + UR * 2 * p + (256 / p) * k) * sizeof(float);
   static const hipError_t attr = hipFuncSetAttribute(
       (const void*)rr_update_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)((128 * 128 + UR * 256 + 16 * 128) * sizeof(float)));
   DEIG_HIP_CHECK(attr);
-  hipLaunchKernelGGL(rr_update_kernel, dim3(nblk), dim3(256), shm, stream, b.Z, d, p, k, b.W,
-                     b.lam, b.cs, b.qs, V, ldv, b.resid_part);
+  hipLaunchKernelGGL(rr_update_kernel, dim3(nblk, pbt.n), dim3(256), shm, stream, b.Z, d, p, k, b.W,
+                     b.lam, b.cs, b.qs, ldv, b.resid_part, pbt);
   DEIG_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(rr_finish_kernel, dim3(1), dim3(256), 0, stream, b.resid_part, nblk, k, b.lam,
-                     evals, b.resid);
+  hipLaunchKernelGGL(rr_finish_kernel, dim3(pbt.n), dim3(256), 0, stream, b.resid_part, nblk, k,
+                     b.lam, b.resid, pbt);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }

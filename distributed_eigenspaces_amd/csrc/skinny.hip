@@ -39,8 +39,15 @@ __global__ __launch_bounds__(ST) void skinny_kernel(const float* __restrict__ A,
                                                     const float* __restrict__ B, int64_t ldb,
                                                     float* __restrict__ C, int64_t ldc,
                                                     int64_t M, int64_t K, float alpha, float beta,
-                                                    float* __restrict__ part) {
+                                                    float* __restrict__ part, const ProbBatch pbt) {
   constexpr int N = NB * 16;
+  if (const int prob = blockIdx.z) {  // batched: problem blockIdx.z's operands
+    const int64_t o = pbt.off[prob];
+    A = reinterpret_cast<const float*>(reinterpret_cast<const char*>(A) + o);
+    B = reinterpret_cast<const float*>(reinterpret_cast<const char*>(B) + o);
+    C = reinterpret_cast<float*>(reinterpret_cast<char*>(C) + o);
+    part = reinterpret_cast<float*>(reinterpret_cast<char*>(part) + o);
+  }
   constexpr int BST = bstride(N);
   constexpr int NB4 = SBK * N / 4;                 // float4s of a B chunk
   constexpr int BPT = (NB4 + ST - 1) / ST;         // per thread
@@ -173,8 +180,12 @@ template <int V>
 __global__ __launch_bounds__(256) void skinny_reduce_kernel(const float* __restrict__ part, int ks,
                                                             float* __restrict__ C, int64_t ldc,
                                                             int64_t M, int N, float alpha,
-                                                            float beta) {
+                                                            float beta, const ProbBatch pbt) {
   using fv = std::conditional_t<V == 1, float, f32x4>;
+  if (const int prob = blockIdx.y) {
+    part = reinterpret_cast<const float*>(reinterpret_cast<const char*>(part) + pbt.off[prob]);
+    C = reinterpret_cast<float*>(reinterpret_cast<char*>(C) + pbt.off[prob]);
+  }
   const int64_t idx = ((int64_t)blockIdx.x * 256 + threadIdx.x) * V;
   if (idx >= M * N) return;
   const int64_t m = idx / N;
@@ -190,16 +201,16 @@ __global__ __launch_bounds__(256) void skinny_reduce_kernel(const float* __restr
 template <int NB, bool TRANS>
 int launch_nb(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
               int64_t M, int64_t K, float alpha, float beta, float* part, int ks,
-              hipStream_t st) {
+              hipStream_t st, const ProbBatch& pbt) {
   constexpr int N = NB * 16;
   const size_t shm = (size_t)(2 * SBK * AST + 2 * SBK * bstride(N)) * sizeof(float);
   // once per instantiation (C++11 thread-safe static initialisation)
   static const hipError_t attr = hipFuncSetAttribute(
       (const void*)skinny_kernel<NB, TRANS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   DEIG_HIP_CHECK(attr);
-  dim3 grid((unsigned)cdiv(M, SBM), (unsigned)ks);
+  dim3 grid((unsigned)cdiv(M, SBM), (unsigned)ks, (unsigned)pbt.n);
   hipLaunchKernelGGL((skinny_kernel<NB, TRANS>), grid, dim3(ST), shm, st, A, lda, B, ldb, C, ldc,
-                     M, K, alpha, beta, part);
+                     M, K, alpha, beta, part, pbt);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }
@@ -207,11 +218,11 @@ int launch_nb(const float* A, int64_t lda, const float* B, int64_t ldb, float* C
 template <bool TRANS>
 int launch_t(int NB, const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
              int64_t ldc, int64_t M, int64_t K, float alpha, float beta, float* part, int ks,
-             hipStream_t st) {
+             hipStream_t st, const ProbBatch& pbt) {
   switch (NB) {
 #define DEIG_NB(x) \
   case x:          \
-    return launch_nb<x, TRANS>(A, lda, B, ldb, C, ldc, M, K, alpha, beta, part, ks, st);
+    return launch_nb<x, TRANS>(A, lda, B, ldb, C, ldc, M, K, alpha, beta, part, ks, st, pbt);
     DEIG_NB(1) DEIG_NB(2) DEIG_NB(3) DEIG_NB(4) DEIG_NB(5) DEIG_NB(6) DEIG_NB(7) DEIG_NB(8)
     DEIG_NB(9) DEIG_NB(10) DEIG_NB(11) DEIG_NB(12) DEIG_NB(13) DEIG_NB(14) DEIG_NB(15)
     DEIG_NB(16)
@@ -246,9 +257,12 @@ size_t skinny_workspace_bytes(int64_t M, int64_t N, int64_t K) {
 
 int skinny_launch(bool trans_a, const float* A, int64_t lda, const float* B, int64_t ldb,
                   float* C, int64_t ldc, int64_t M, int64_t N, int64_t K, float alpha,
-                  float beta, float* slab, size_t slab_bytes, hipStream_t stream) {
+                  float beta, float* slab, size_t slab_bytes, hipStream_t stream,
+                  const ProbBatch* batch) {
   DEIG_REQUIRE(N >= 16 && N <= 256 && N % 16 == 0, "skinny: N=%lld must be 16..256, %%16",
                (long long)N);
+  const ProbBatch pbt = batch ? *batch : one_problem();
+  DEIG_REQUIRE(pbt.n >= 1 && pbt.n <= kMaxProbBatch && pbt.off[0] == 0, "skinny: batch of %d", pbt.n);
   DEIG_REQUIRE(M >= 1 && K >= 1, "skinny: empty problem");
   DEIG_REQUIRE(lda % 4 == 0 && ldb % 4 == 0 && ldb >= N && ldc >= N, "skinny: bad leading dims");
   DEIG_REQUIRE(aligned16(A) && aligned16(B), "skinny: A, B must be 16-byte aligned");
@@ -260,18 +274,18 @@ int skinny_launch(bool trans_a, const float* A, int64_t lda, const float* B, int
   const size_t need = ks > 1 ? (size_t)ks * M * N * sizeof(float) : 0;
   if (slab_bytes < need) return fail(DEIG_EWORKSPACE, "skinny: slab %zu < %zu", slab_bytes, need);
   const int NB = (int)(N / 16);
-  int rc = trans_a ? launch_t<true>(NB, A, lda, B, ldb, C, ldc, M, K, alpha, beta, slab, ks, stream)
+  int rc = trans_a ? launch_t<true>(NB, A, lda, B, ldb, C, ldc, M, K, alpha, beta, slab, ks, stream, pbt)
                    : launch_t<false>(NB, A, lda, B, ldb, C, ldc, M, K, alpha, beta, slab, ks,
-                                     stream);
+                                     stream, pbt);
   if (rc) return rc;
   if (ks > 1) {
     const int64_t tot = M * N;
     if (ldc % 4 == 0 && aligned16(C))
-      hipLaunchKernelGGL(skinny_reduce_kernel<4>, dim3((unsigned)cdiv(tot / 4, 256)), dim3(256), 0,
-                         stream, slab, ks, C, ldc, M, (int)N, alpha, beta);
+      hipLaunchKernelGGL(skinny_reduce_kernel<4>, dim3((unsigned)cdiv(tot / 4, 256), (unsigned)pbt.n),
+                         dim3(256), 0, stream, slab, ks, C, ldc, M, (int)N, alpha, beta, pbt);
     else
-      hipLaunchKernelGGL(skinny_reduce_kernel<1>, dim3((unsigned)cdiv(tot, 256)), dim3(256), 0,
-                         stream, slab, ks, C, ldc, M, (int)N, alpha, beta);
+      hipLaunchKernelGGL(skinny_reduce_kernel<1>, dim3((unsigned)cdiv(tot, 256), (unsigned)pbt.n),
+                         dim3(256), 0, stream, slab, ks, C, ldc, M, (int)N, alpha, beta, pbt);
     DEIG_HIP_CHECK(hipGetLastError());
   }
   return DEIG_OK;

@@ -78,8 +78,14 @@ __device__ __forceinline__ f32x4 mfma16(const u32x4& a, const u32x4& b, const f3
 template <int NP>
 __global__ __launch_bounds__(256) void split_q_kernel(float* __restrict__ Q, int64_t ldq,
                                                       int64_t d, int nb, int64_t ngrp,
-                                                      u32x4* __restrict__ QS) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+                                                      u32x4* __restrict__ QS, int per,
+                                                      const SweepBatch sb) {
+  const int prob = blockIdx.x / per;
+  if (prob) {
+    Q = reinterpret_cast<float*>(reinterpret_cast<char*>(Q) + sb.off[prob]);
+    QS = reinterpret_cast<u32x4*>(reinterpret_cast<char*>(QS) + sb.off[prob]);
+  }
+  const int64_t idx = (int64_t)(blockIdx.x - prob * per) * 256 + threadIdx.x;
   if (idx >= ngrp * nb * 64) return;
   const int lane = (int)(idx & 63);
   const int64_t t = idx >> 6;  // g * nb + j
@@ -249,19 +255,35 @@ __global__ __launch_bounds__(256) void sweep_prepare_kernel(const T* __restrict_
 // drops the MFMAs, bit 1 the S loads, bit 2 the Q loads (results are garbage).
 // PRE: SI is the two-piece image (sweep_prepare_kernel's SH: h | m per half slot)
 // and the products are the three of SP = 2 - the early-sweep mode, no split.
+// per / sb (every sweep kernel): one launch may cover sb.n problems of the same shape
+// (the batched worker solves, capi.hip solve_batch): logical blocks [i per, (i + 1) per)
+// are problem i's, and every pointer of problem i is problem 0's plus sb.off[i] bytes
+// (the solver workspaces are equally carved slices of one allocation).  One problem:
+// per = the grid, sb.n = 1.
 template <int NB, int NP, int PROBE = 0, bool PRE = false>
 __global__ __launch_bounds__(256, 1) void sweep2_kernel(const f32x4* __restrict__ SI, int64_t d,
                                                         const u32x4* __restrict__ QS,
                                                         int64_t ngrp, float* __restrict__ Y,
                                                         int64_t ldy, float alpha,
-                                                        float* __restrict__ part) {
+                                                        float* __restrict__ part, int per,
+                                                        const SweepBatch sb) {
   constexpr int MB = 4;
+  // logical block ids are XCD-contiguous (xcd_logical), so one problem's blocks share
+  // an XCD's L2
+  const int gl = xcd_logical(blockIdx.x, gridDim.x);
+  const int prob = gl / per, lid = gl - prob * per;
+  if (prob) {
+    const int64_t po = sb.off[prob];
+    SI = reinterpret_cast<const f32x4*>(reinterpret_cast<const char*>(SI) + po);
+    QS = reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(QS) + po);
+    Y = reinterpret_cast<float*>(reinterpret_cast<char*>(Y) + po);
+    part = reinterpret_cast<float*>(reinterpret_cast<char*>(part) + po);
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, gq = lane >> 4;
   const int bx = (int)cdiv(d, SI_BR);
-  const int ks = (int)(gridDim.x / bx);
-  const int lid = xcd_logical(blockIdx.x, gridDim.x);
+  const int ks = per / bx;
   const int sl = lid / bx;
   const int64_t rb = (int64_t)(lid - sl * bx) * (SI_BR / SI_RB) + wave;
   const int64_t row0 = rb * SI_RB;
@@ -404,7 +426,8 @@ __global__ __launch_bounds__(256, 1) void sweep2_kernel(const f32x4* __restrict_
 // those covers it); the slot refilled at group g was last read at g - 1.
 __device__ __forceinline__ void sw_dma16(const __amdgpu_buffer_rsrc_t rsrc, int voff,
                                          const void* lds_dst) {
-  const unsigned m0v = (unsigned)(uintptr_t)(lds_void*)lds_dst;
+  // uniform, but the compiler may compute it in VGPRs (packed 16-bit slot arithmetic)
+  const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)lds_dst);
   asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
                :
                : "v"(voff), "s"(rsrc), "s"(m0v)
@@ -433,7 +456,19 @@ __global__ __launch_bounds__(256, OCC) void sweep3_kernel(const f32x4* __restric
                                                         const u32x4* __restrict__ QS,
                                                         int64_t ngrp, float* __restrict__ Y,
                                                         int64_t ldy, float alpha,
-                                                        float* __restrict__ part) {
+                                                        float* __restrict__ part, int per,
+                                                        const SweepBatch sb) {
+  // logical block ids are XCD-contiguous (xcd_logical), so one problem's blocks share
+  // an XCD's L2
+  const int gl = xcd_logical(blockIdx.x, gridDim.x);
+  const int prob = gl / per, lid = gl - prob * per;
+  if (prob) {
+    const int64_t po = sb.off[prob];
+    SI = reinterpret_cast<const f32x4*>(reinterpret_cast<const char*>(SI) + po);
+    QS = reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(QS) + po);
+    Y = reinterpret_cast<float*>(reinterpret_cast<char*>(Y) + po);
+    part = reinterpret_cast<float*>(reinterpret_cast<char*>(part) + po);
+  }
   constexpr int MB = MBW;
   static_assert(MB == 2 || MB == 4, "m-blocks per wave");
   constexpr int U = NP * NB;         // 1-KiB Q pieces per k-group
@@ -446,8 +481,7 @@ __global__ __launch_bounds__(256, OCC) void sweep3_kernel(const f32x4* __restric
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, gq = lane >> 4;
   const int bx = (int)cdiv(d, 4 * 16 * MB);
-  const int ks = (int)(gridDim.x / bx);
-  const int lid = xcd_logical(blockIdx.x, gridDim.x);
+  const int ks = per / bx;
   const int sl = lid / bx;
   const int64_t rb = (int64_t)(lid - sl * bx) * 4 + wave;  // this wave's 16 MB rows
   const int64_t row0 = rb * 16 * MB;
@@ -546,9 +580,15 @@ __global__ __launch_bounds__(256, OCC) void sweep3_kernel(const f32x4* __restric
 template <int V>
 __global__ __launch_bounds__(256) void sweep_reduce_kernel(const float* __restrict__ part, int ks,
                                                            int64_t d, int p, float alpha,
-                                                           float* __restrict__ Y, int64_t ldy) {
+                                                           float* __restrict__ Y, int64_t ldy, int per,
+                                                           const SweepBatch sb) {
   using fv = std::conditional_t<V == 1, float, f32x4>;
-  const int64_t idx = ((int64_t)blockIdx.x * 256 + threadIdx.x) * V;
+  const int prob = blockIdx.x / per, bid = blockIdx.x - prob * per;
+  if (prob) {
+    part = reinterpret_cast<const float*>(reinterpret_cast<const char*>(part) + sb.off[prob]);
+    Y = reinterpret_cast<float*>(reinterpret_cast<char*>(Y) + sb.off[prob]);
+  }
+  const int64_t idx = ((int64_t)bid * 256 + threadIdx.x) * V;
   if (idx >= d * p) return;
   const int64_t m = idx / p;
   const int n = (int)(idx - m * p);
@@ -572,10 +612,30 @@ __global__ __launch_bounds__(256) void sweep_finish_kernel(const float* __restri
                                                            int64_t d, int p, float alpha,
                                                            float* __restrict__ Y, int64_t ldy,
                                                            SweepStep st, int nb,
-                                                           u32x4* __restrict__ QS) {
+                                                           u32x4* __restrict__ QS, int per,
+                                                           const SweepBatch sb) {
   __shared__ float qt[8][132];
-  const int64_t g = blockIdx.x >> 2;
-  const int o = blockIdx.x & 3;
+  const int prob = blockIdx.x / per, bid = blockIdx.x - prob * per;
+  if (prob) {
+    const int64_t po = sb.off[prob];
+    part = reinterpret_cast<const float*>(reinterpret_cast<const char*>(part) + po);
+    Y = reinterpret_cast<float*>(reinterpret_cast<char*>(Y) + po);
+    QS = reinterpret_cast<u32x4*>(reinterpret_cast<char*>(QS) + po);
+    st.Q = reinterpret_cast<float*>(reinterpret_cast<char*>(st.Q) + po);
+    st.T = reinterpret_cast<float*>(reinterpret_cast<char*>(st.T) + po);
+    st.cs = reinterpret_cast<const float*>(reinterpret_cast<const char*>(st.cs) + po);
+    st.lam = reinterpret_cast<const float*>(reinterpret_cast<const char*>(st.lam) + po);
+  }
+  if (sb.n > 1) {  // this problem's own step constants
+    st.kind = sb.kind[prob];
+    st.tau = sb.tau[prob];
+    st.thr = sb.thr[prob];
+    st.a = sb.a[prob];
+    st.cc = sb.cc[prob];
+    st.gamma = sb.gamma[prob];
+  }
+  const int64_t g = bid >> 2;
+  const int o = bid & 3;
   const int pq = p >> 2;
   const int u = threadIdx.x;
   if (u < 8 * pq) {
@@ -685,30 +745,37 @@ int sweep_ks_mb(int64_t d, int mb) {
 // Q image: 3 bf16 pieces per value
 size_t qs_bytes(int64_t d, int p) { return (size_t)cdiv(d, SW_KS) * SW_KS * p * 6; }
 
+// One launch: sb.n problems of `per` blocks each.
+struct Grid {
+  int per;
+  const SweepBatch* sb;
+  dim3 dim() const { return dim3((unsigned)(per * sb->n)); }
+};
+
 template <int NB, int NP, bool PRE>
-void launch_v2(dim3 grid, hipStream_t st, const f32x4* SI, int64_t d, const u32x4* QS, float* Y,
+void launch_v2(Grid g, hipStream_t st, const f32x4* SI, int64_t d, const u32x4* QS, float* Y,
                int64_t ldy, float alpha, float* part) {
   const int64_t ng = si_groups(d);
-  hipLaunchKernelGGL((sweep2_kernel<NB, NP, 0, PRE>), grid, dim3(256), 0, st, SI, d, QS, ng, Y,
-                     ldy, alpha, part);
+  hipLaunchKernelGGL((sweep2_kernel<NB, NP, 0, PRE>), g.dim(), dim3(256), 0, st, SI, d, QS, ng, Y,
+                     ldy, alpha, part, g.per, *g.sb);
 }
 
 template <int NB, int NP, bool PRE>
-void launch_v3(dim3 grid, hipStream_t st, const f32x4* SI, int64_t d, const u32x4* QS, float* Y,
+void launch_v3(Grid g, hipStream_t st, const f32x4* SI, int64_t d, const u32x4* QS, float* Y,
                int64_t ldy, float alpha, float* part) {
   const int64_t ng = si_groups(d);
   if (sweep_mb(PRE, NB) == 2)
-    hipLaunchKernelGGL((sweep3_kernel<NB, NP, kSweepDepth, 1, PRE, 2>), grid, dim3(256), 0, st, SI,
-                       d, QS, ng, Y, ldy, alpha, part);
+    hipLaunchKernelGGL((sweep3_kernel<NB, NP, kSweepDepth, 1, PRE, 2>), g.dim(), dim3(256), 0, st,
+                       SI, d, QS, ng, Y, ldy, alpha, part, g.per, *g.sb);
   else
-    hipLaunchKernelGGL((sweep3_kernel<NB, NP, kSweepDepth, 1, PRE>), grid, dim3(256), 0, st, SI, d,
-                       QS, ng, Y, ldy, alpha, part);
+    hipLaunchKernelGGL((sweep3_kernel<NB, NP, kSweepDepth, 1, PRE>), g.dim(), dim3(256), 0, st, SI,
+                       d, QS, ng, Y, ldy, alpha, part, g.per, *g.sb);
 }
 
 // v2 (sweep3 = false) or v3 with NP Q pieces, NB = p / 16 column blocks; PRE: the
 // two-piece S image (three products).
 template <int NP, bool PRE = false>
-void launch_image(bool v3, int nb, dim3 grid, hipStream_t st, const f32x4* SI, int64_t d,
+void launch_image(bool v3, int nb, Grid grid, hipStream_t st, const f32x4* SI, int64_t d,
                   const u32x4* QS, float* Y, int64_t ldy, float alpha, float* part) {
 #define DEIG_NB_CASE(N_)                                                   \
   case N_:                                                                 \
@@ -784,7 +851,12 @@ int sweep_prepare(const void* S, int stype, int64_t d, int64_t lds, int p, void*
 
 int sweep_apply(const float* Q, int64_t d, int p, int64_t ldq, float* Y, int64_t ldy, float alpha,
                 void* ws, size_t ws_bytes, hipStream_t st, int mode, const SweepStep* step,
-                bool q_ready, bool kernel_only) {
+                bool q_ready, bool kernel_only, const SweepBatch* batch) {
+  SweepBatch one{};
+  one.n = 1;
+  const SweepBatch* sb = batch ? batch : &one;
+  DEIG_REQUIRE(sb->n >= 1 && sb->n <= kMaxSweepBatch && sb->off[0] == 0,
+               "sweep: batch of %d problems (1..%d, off[0] = 0)", sb->n, kMaxSweepBatch);
   const bool round_q = mode >= 1;
   DEIG_REQUIRE(d >= 1 && p >= 16 && p <= 128 && p % 16 == 0,
                "sweep: need d >= 1 and p in {16, 32, ..., 128} (p=%d)", p);
@@ -801,11 +873,11 @@ int sweep_apply(const float* Q, int64_t d, int p, int64_t ldq, float* Y, int64_t
   // q_ready: the previous sweep's finish kernel already wrote this Q's image
   if (!q_ready) {
     if (np == 2)
-      hipLaunchKernelGGL(split_q_kernel<2>, qgrid, dim3(256), 0, st, const_cast<float*>(Q), ldq, d,
-                         nb, ngrp, w.QS);
+      hipLaunchKernelGGL(split_q_kernel<2>, dim3(qgrid.x * sb->n), dim3(256), 0, st,
+                         const_cast<float*>(Q), ldq, d, nb, ngrp, w.QS, (int)qgrid.x, *sb);
     else
-      hipLaunchKernelGGL(split_q_kernel<3>, qgrid, dim3(256), 0, st, const_cast<float*>(Q), ldq, d,
-                         nb, ngrp, w.QS);
+      hipLaunchKernelGGL(split_q_kernel<3>, dim3(qgrid.x * sb->n), dim3(256), 0, st,
+                         const_cast<float*>(Q), ldq, d, nb, ngrp, w.QS, (int)qgrid.x, *sb);
     DEIG_HIP_CHECK(hipGetLastError());
   }
   // v3 (LDS-shared Q ring): above p = 80 (v2's register rings spill) and for the
@@ -815,8 +887,12 @@ int sweep_apply(const float* Q, int64_t d, int p, int64_t ldq, float* Y, int64_t
   // split in the sweep)
   const bool v3 = nb > 5 || (pre && nb >= 4);
   const int mbw = v3 ? sweep_mb(pre, nb) : 4;
+  const int64_t bx = cdiv(d, mbw == 4 ? SI_BR : 64 * mbw);
+  // a batch keeps the single problem's slicing: bit-identical to separate solves (and
+  // fewer slices for a batch that fills the chip measured no faster: c1 7.85 vs 7.85,
+  // c1g 14.9 vs 15.3 M samples/s, profiles/r04f_bench_*)
   const int ks = sweep_ks_mb(d, mbw);
-  const dim3 grid((unsigned)(cdiv(d, mbw == 4 ? SI_BR : 64 * mbw) * ks));
+  const Grid grid{(int)(bx * ks), sb};
   if (pre)
     launch_image<2, true>(v3, nb, grid, st, reinterpret_cast<const f32x4*>(w.SH), d, w.QS, Y, ldy,
                           alpha, w.part);
@@ -832,23 +908,27 @@ int sweep_apply(const float* Q, int64_t d, int p, int64_t ldq, float* Y, int64_t
                  "sweep: fused step needs 16-byte aligned Y / Q rows");
     const int nnp = step->next_mode >= kSweepRoundQ ? kRoundPieces : 3;
     const float* pp = ks > 1 ? w.part : nullptr;
-    const dim3 fgrid((unsigned)(4 * ngrp)), fblk((unsigned)((2 * p + 63) / 64 * 64));
+    const int fper = (int)(4 * ngrp);
+    const dim3 fgrid((unsigned)(fper * sb->n)), fblk((unsigned)((2 * p + 63) / 64 * 64));
     if (nnp == 2)
       hipLaunchKernelGGL(sweep_finish_kernel<2>, fgrid, fblk, 0, st, pp, ks, d, p, alpha, Y, ldy,
-                         *step, nb, w.QS);
+                         *step, nb, w.QS, fper, *sb);
     else
       hipLaunchKernelGGL(sweep_finish_kernel<3>, fgrid, fblk, 0, st, pp, ks, d, p, alpha, Y, ldy,
-                         *step, nb, w.QS);
+                         *step, nb, w.QS, fper, *sb);
     DEIG_HIP_CHECK(hipGetLastError());
     return DEIG_OK;
   }
   if (ks > 1) {
-    if (ldy % 4 == 0 && aligned16(Y))
-      hipLaunchKernelGGL(sweep_reduce_kernel<4>, dim3((unsigned)cdiv(d * p / 4, 256)), dim3(256),
-                         0, st, w.part, ks, d, p, alpha, Y, ldy);
-    else
-      hipLaunchKernelGGL(sweep_reduce_kernel<1>, dim3((unsigned)cdiv(d * p, 256)), dim3(256), 0,
-                         st, w.part, ks, d, p, alpha, Y, ldy);
+    if (ldy % 4 == 0 && aligned16(Y)) {
+      const int rper = (int)cdiv(d * p / 4, 256);
+      hipLaunchKernelGGL(sweep_reduce_kernel<4>, dim3((unsigned)(rper * sb->n)), dim3(256), 0, st,
+                         w.part, ks, d, p, alpha, Y, ldy, rper, *sb);
+    } else {
+      const int rper = (int)cdiv(d * p, 256);
+      hipLaunchKernelGGL(sweep_reduce_kernel<1>, dim3((unsigned)(rper * sb->n)), dim3(256), 0, st,
+                         w.part, ks, d, p, alpha, Y, ldy, rper, *sb);
+    }
     DEIG_HIP_CHECK(hipGetLastError());
   }
   return DEIG_OK;

@@ -382,31 +382,15 @@ def topk_eigh(S: torch.Tensor, k: int, *, p: int | None = None, tol: float = DEF
     return _finish(rc, V, evals, sweeps, resid, "deig_topk_sym_ex")
 
 
-_batch_streams = threading.local()
-
-
-def _side_streams(device: torch.device, n: int):
-    """n HIP streams of this thread for the batched solver's per-problem work (kept:
-    creating streams per call would cost more than the solves at small d)."""
-    key = device.index
-    pool = getattr(_batch_streams, "pools", None)
-    if pool is None:
-        pool = _batch_streams.pools = {}
-    lst = pool.setdefault(key, [])
-    while len(lst) < n:
-        lst.append(torch.cuda.Stream(device))
-    return lst[:n]
-
-
 def topk_eigh_batch(Ss, k: int, *, p: int | None = None, tol: float = DEFAULT_TOL,
                     max_sweeps: int = DEFAULT_MAX_SWEEPS, check_finite: bool = True,
                     opts: "_lib.SolverOpts | None" = None) -> list:
     """``topk_eigh`` of W same-shape symmetric matrices at once (the logical workers
     of one GPU, each SlaveNode's top_k_eigenvectors of distributed.py:22-29,
-    :42-53): the same results as W ``topk_eigh`` calls, with the small
-    Rayleigh-Ritz solves of all W problems in one launch per step and each problem's
-    sweeps on its own stream (include/deig.h deig_topk_sym_batch).  Returns a list
-    of EigResult; the work is joined into the current stream."""
+    :42-53): the same results as W ``topk_eigh`` calls, the W problems advanced in
+    lockstep on the current stream with each step's sweeps, Grams, small
+    Rayleigh-Ritz solves and updates batched across them (include/deig.h
+    deig_topk_sym_batch).  Returns a list of EigResult."""
     Ss = [require_device_tensor(S, "topk_eigh_batch", keep_f64=True) for S in Ss]
     if not Ss:
         return []
@@ -441,20 +425,13 @@ def topk_eigh_batch(Ss, k: int, *, p: int | None = None, tol: float = DEFAULT_TO
     V_arr = (vp * W)(*[V.data_ptr() for V in Vs])
     E_arr = (vp * W)(*[e.data_ptr() for e in evs])
     cur = torch.cuda.current_stream(dev)
-    side = _side_streams(dev, W)
-    for s in side:  # every problem's stream starts behind the caller's stream
-        s.wait_stream(cur)
-    st_arr = (vp * W)(*[s.cuda_stream for s in side])
     L = _lib.lib()
     with torch.cuda.device(dev):
         nbytes = L.deig_topk_batch_workspace(W, d, k, pp, stype, ctypes.byref(o))
         ws = _workspace(dev, nbytes)
         rc = L.deig_topk_sym_batch(W, S_arr, stype, d, lds, k, pp, int(max_sweeps), ctypes.c_float(tol),
                                    V_arr, d, E_arr, sweeps, resid, status, ctypes.byref(o),
-                                   ws.data_ptr(), nbytes, st_arr, cur.cuda_stream)
-    for t in mats + Vs + evs:  # used on the side streams
-        for s in side:
-            t.record_stream(s)
+                                   ws.data_ptr(), nbytes, None, cur.cuda_stream)
     _lib.check(rc, "deig_topk_sym_batch")
     if rc != _lib.DEIG_OK:
         warnings.warn(f"deig_topk_sym_batch: {_lib.last_error()}", _lib.NotConvergedWarning, stacklevel=2)

@@ -258,11 +258,12 @@ int deig_projavg_topk_f32(const float* Wt, int64_t d, int64_t mk, int64_t ldw,
  * element type; S[i] row-major with leading dimension lds, 16-byte aligned),
  * advanced in lockstep: equivalent to W deig_topk_sym_ex calls with the same
  * options (same kernels, same decisions; V[i] column-major with ldv, evals[i]
- * ascending, sweeps_out[i] / resid_out[i] as there), but the small Rayleigh-Ritz
- * solves of all problems run in one launch per step (one workgroup each) instead
- * of W streams contending for the hardware queues.  streams[i]: problem i's stream
- * for its sweeps and updates (NULL array or entries: `stream`); the batched small
- * solves run on `stream`, and on return every problem's work has been joined into
+ * ascending, sweeps_out[i] / resid_out[i] as there), but each step of all problems
+ * is enqueued as batched launches on `stream` (the sweeps of all problems at the same
+ * point of their plans in one launch per kernel, one Gram, one small-solve launch of
+ * one workgroup per problem, one update) and one stream sync serves every problem's
+ * host decisions.  streams: ignored since 0x000400 (r03: per-problem streams; kept
+ * for the ABI, may be NULL).  All work is ordered on
  * `stream`.  Workspace: deig_topk_batch_workspace(W, ...) bytes.  Returns the
  * first error; DEIG_NOT_CONVERGED if any problem stopped above tol.  status_out[i]
  * (host array, may be NULL): problem i's own return code, the one deig_topk_sym_ex
