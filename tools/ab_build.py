@@ -2,7 +2,7 @@
 recompiled with it, the rest linked from the in-tree build (measurement tooling; the
 shipped library has no knobs).
 
-  python tools/ab_build.py DEIG_AB_BATCH_KS tools/ab_libs/libdeig_batchks.so
+  python tools/ab_build.py DEIG_AB_SYRK_PIPE=1 tools/ab_libs/libdeig_pipe1.so
 """
 import os
 import subprocess
@@ -21,7 +21,7 @@ def build(macro, out):
     objs = []
     for s in _build.SOURCES:
         src = os.path.join(_build.CSRC, s)
-        if macro in open(src).read():
+        if macro.split("=")[0] in open(src).read():
             obj = f"{out}.{s}.o"
             subprocess.run([hipcc, f"--offload-arch={_build.ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
                             "-Wno-unused-function", "-Wno-inline-asm", f"-D{macro}", "-c", src, "-o", obj],
