@@ -793,19 +793,10 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
   }
   __syncthreads();
   const int tr0 = tid / half, tc0 = tid - tr0 * half;
+#ifdef DEIG_AB_RR_JOLD
   const int dq = NT / half, dr = NT - dq * half;
-#ifdef DEIG_AB_RR_JLOW
-  // A/B: only the lower slot blocks (tr >= tc) are rotated, each writing its mirror
-  constexpr int MI = (64 * 65 / 2 + NT - 1) / NT;
-  const int nitems = half * (half + 1) / 2;
-  int itr[MI], itc[MI];
-#pragma unroll
-  for (int u = 0; u < MI; ++u) {
-    int r = 0, c = 0;
-    if (tid + u * NT < nitems) tri_rc(tid + u * NT, r, c);
-    itr[u] = r;
-    itc[u] = c;
-  }
+#else
+  const int cpt = NT / half;
 #endif
   for (int sw = 0; sw < max_jsweeps; ++sw) {
     if (tid == 0) nrot[0] = 0;
@@ -854,34 +845,7 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
       __syncthreads();
       const int step_rot = nrot[ci];
       if (step_rot != 0) {
-#ifdef DEIG_AB_RR_JLOW
-#pragma unroll
-        for (int u = 0; u < MI; ++u) {
-          if (tid + u * NT >= nitems) break;
-          const int tr = itr[u], tc = itc[u];
-          const f32x4 qr = rotp[tr], qc = rotp[tc];
-          const int ar = __float_as_int(qr[2]), br = __float_as_int(qr[3]);
-          const int ac = __float_as_int(qc[2]), bc = __float_as_int(qc[3]);
-          const float cr = qr[0], sr = qr[1], cc = qc[0], sc = qc[1];
-          const float x = X1[ar * p + ac], y = X1[ar * p + bc];
-          const float z = X1[br * p + ac], w = X1[br * p + bc];
-          const float x1 = cc * x - sc * y, y1 = sc * x + cc * y;
-          const float z1 = cc * z - sc * w, w1 = sc * z + cc * w;
-          const float nx = cr * x1 - sr * z1, nz = sr * x1 + cr * z1;
-          const float ny = cr * y1 - sr * w1, nw = sr * y1 + cr * w1;
-          X1[ar * p + ac] = nx;
-          X1[br * p + ac] = nz;
-          X1[ar * p + bc] = ny;
-          X1[br * p + bc] = nw;
-          if (tr != tc) {
-            X1[ac * p + ar] = nx;
-            X1[ac * p + br] = nz;
-            X1[bc * p + ar] = ny;
-            X1[bc * p + br] = nw;
-          }
-        }
-        int tr = tr0, tc = tc0;
-#else
+#ifdef DEIG_AB_RR_JOLD
         int tr = tr0, tc = tc0;
         for (int idx = tid; idx < half * half; idx += NT) {
           const f32x4 qr = rotp[tr], qc = rotp[tc];
@@ -903,7 +867,6 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
             ++tr;
           }
         }
-#endif
         tr = tr0;
         tc = tc0;
         for (int idx = tid; idx < p * half; idx += NT) {
@@ -921,6 +884,34 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
           X2[r * p + a] = c * va - s * vb;
           X2[r * p + b] = s * va + c * vb;
         }
+#else
+        // thread -> column pair tc0 and every cpt-th row pair (and V row): the column
+        // pair's rotation record is read once per step instead of once per 2 x 2 block
+        // and V item (the step is LDS-bound: at p = 128, 524 -> 360 KB per step)
+        if (tid < cpt * half) {
+          const f32x4 qc = rotp[tc0];
+          const int ac = __float_as_int(qc[2]), bc = __float_as_int(qc[3]);
+          const float cc = qc[0], sc = qc[1];
+          for (int tr = tr0; tr < half; tr += cpt) {
+            const f32x4 qr = rotp[tr];
+            const int ar = __float_as_int(qr[2]), br = __float_as_int(qr[3]);
+            const float cr = qr[0], sr = qr[1];
+            const float x = X1[ar * p + ac], y = X1[ar * p + bc];
+            const float z = X1[br * p + ac], w = X1[br * p + bc];
+            const float x1 = cc * x - sc * y, y1 = sc * x + cc * y;
+            const float z1 = cc * z - sc * w, w1 = sc * z + cc * w;
+            X1[ar * p + ac] = cr * x1 - sr * z1;
+            X1[br * p + ac] = sr * x1 + cr * z1;
+            X1[ar * p + bc] = cr * y1 - sr * w1;
+            X1[br * p + bc] = sr * y1 + cr * w1;
+          }
+          for (int r = tr0; r < p; r += cpt) {
+            const float va = X2[r * p + ac], vb = X2[r * p + bc];
+            X2[r * p + ac] = cc * va - sc * vb;
+            X2[r * p + bc] = sc * va + cc * vb;
+          }
+        }
+#endif
       }
       __syncthreads();
       if (tid == 0) {

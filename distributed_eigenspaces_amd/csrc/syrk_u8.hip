@@ -74,10 +74,19 @@ __global__ __launch_bounds__(PREP_THR) void u8_prep_kernel(const uint8_t* __rest
                                                            int64_t n, int64_t ldx, int d,
                                                            int64_t fpad, int64_t nkb,
                                                            uint8_t* __restrict__ img,
-                                                           unsigned long long* __restrict__ colsum) {
+                                                           unsigned long long* __restrict__ colsum,
+                                                           int nt, int* __restrict__ order) {
   constexpr int NP = MODE == DEIG_U8_GRAY3 ? 3 : 1;
   __shared__ long long cs[4][256];
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  if (blockIdx.x == 0 && blockIdx.y == 0) {  // the tile order: lower triangle, row-major
+    for (int i = threadIdx.x; i < nt * (nt + 1) / 2; i += PREP_THR) {
+      int ti = (int)((sqrtf(8.f * (float)i + 1.f) - 1.f) * 0.5f);
+      while (ti * (ti + 1) / 2 > i) --ti;
+      while ((ti + 1) * (ti + 2) / 2 <= i) ++ti;
+      order[i] = ti | ((i - ti * (ti + 1) / 2) << 16);
+    }
+  }
   const int f = blockIdx.x * 256 + lane * 4;
   const bool fin = f < d;  // d % 4 == 0: the 4 features are all in or all out
   int csum[4] = {0, 0, 0, 0};
@@ -413,13 +422,6 @@ __global__ __launch_bounds__(256) void u8_finalize_kernel(const unsigned long lo
   if (S64) S64[r * lds64 + c] = v;
 }
 
-__global__ void u8_tile_order_kernel(int nt, int* order) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  int idx = 0;
-  for (int ti = 0; ti < nt; ++ti)
-    for (int tj = 0; tj <= ti; ++tj) order[idx++] = ti | (tj << 16);
-}
-
 struct U8Layout {
   int64_t fpad, nkb, nt, T;
   int planes;
@@ -483,16 +485,14 @@ int syrk_u8_launch(const uint8_t* X, int64_t n, int64_t d, int64_t ldx, int mode
   DEIG_HIP_CHECK(hipMemsetAsync(col, 0, sizeof(unsigned long long) * L.fpad, stream));
   if (!direct)
     DEIG_HIP_CHECK(hipMemsetAsync(G, 0, sizeof(unsigned long long) * L.planes * L.fpad * L.fpad, stream));
-  hipLaunchKernelGGL(u8_tile_order_kernel, dim3(1), dim3(64), 0, stream, (int)L.nt, order);
-  DEIG_HIP_CHECK(hipGetLastError());
   const int yb = (int)(L.nkb < PREP_YB ? L.nkb : PREP_YB);
   const dim3 pg((unsigned)(L.fpad / 256 + (L.fpad % 256 ? 1 : 0)), (unsigned)yb);
   if (mode == DEIG_U8_RAW)
     hipLaunchKernelGGL(u8_prep_kernel<DEIG_U8_RAW>, pg, dim3(PREP_THR), 0, stream, X, n, ldx,
-                       (int)d, L.fpad, L.nkb, img, col);
+                       (int)d, L.fpad, L.nkb, img, col, (int)L.nt, order);
   else
     hipLaunchKernelGGL(u8_prep_kernel<DEIG_U8_GRAY3>, pg, dim3(PREP_THR), 0, stream, X, n, ldx,
-                       (int)d, L.fpad, L.nkb, img, col);
+                       (int)d, L.fpad, L.nkb, img, col, (int)L.nt, order);
   DEIG_HIP_CHECK(hipGetLastError());
   // K segments: enough items to fill the chip twice over, each <= MAX_SEG_KB row
   // blocks (int32 accumulators) and >= 4 (amortise the staging prologue).

@@ -274,16 +274,21 @@ def sigma_hat_u8(x: torch.Tensor, mode: str = "auto", alpha: float | None = None
         x = xx
     if dtype not in (torch.float32, torch.float64):
         raise ValueError("dtype must be torch.float32 or torch.float64")
-    S = torch.empty((dp, dp), dtype=dtype, device=x.device)
+    direct = (out is not None and dp == d and out.dtype == dtype and out.device == x.device
+              and out.shape == (d, d) and out.stride(1) == 1 and out.stride(0) >= d)
+    S = out if direct else torch.empty((dp, dp), dtype=dtype, device=x.device)
     L = _lib.lib()
     with torch.cuda.device(x.device):
         nbytes = L.deig_syrk_u8_workspace(n, dp, _lib.U8_MODES[mode])
         ws = _workspace(x.device, nbytes)
         f32 = dtype == torch.float32
+        lds = S.stride(0)
         rc = L.deig_syrk_u8(x.data_ptr(), n, dp, x.stride(0), _lib.U8_MODES[mode], ctypes.c_double(a),
-                            S.data_ptr() if f32 else None, dp, None if f32 else S.data_ptr(), dp,
+                            S.data_ptr() if f32 else None, lds, None if f32 else S.data_ptr(), lds,
                             ws.data_ptr(), nbytes, _stream(x.device))
     _lib.check(rc, "deig_syrk_u8")
+    if direct:  # written in place
+        return out
     if dp != d:
         S = S[:d, :d].contiguous()
     if out is not None:

@@ -24,7 +24,7 @@ LIBDIR = os.path.join(ROOT, "tools", "ab_libs")
 V1 = os.path.join(LIBDIR, "libdeig_rrv1.so")
 
 
-JLOW = os.path.join(LIBDIR, "libdeig_rrjlow.so")
+SCALARJ = os.path.join(LIBDIR, "libdeig_rrscalarj.so")
 
 
 def build():
@@ -34,7 +34,7 @@ def build():
     objdir = os.path.join(_build.HERE, "build")
     hipcc = _build._hipcc()
     others = [os.path.join(objdir, s.replace(".hip", ".o")) for s in _build.SOURCES if s != "rr.hip"]
-    for define, out in (("-DDEIG_AB_RR_V1", V1), ("-DDEIG_AB_RR_JLOW", JLOW)):
+    for define, out in (("-DDEIG_AB_RR_V1", V1), ("-DDEIG_AB_RR_SCALARJ", SCALARJ)):
         obj = out + ".o"
         subprocess.run([hipcc, f"--offload-arch={_build.ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
                         "-Wno-unused-function", "-Wno-inline-asm", define, "-c",
