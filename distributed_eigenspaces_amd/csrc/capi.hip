@@ -284,6 +284,11 @@ int apply_op(const Operator& op, const SolverWs& w, int64_t d, int p, hipStream_
 // every column); columns whose growth would exceed gmax stay out of the filter
 // (threshold thr on theta_j).  Only used once resid <= cheb_above: before that the
 // Ritz values are too rough to place the interval, and plain power steps run.
+// cheb_above stays 1e-2 (r04 A/B, profiles/r04k_solver_opts_sweep.log and r04m_*): 0.1
+// cut synthetic worker solves 6-16 % (c5 18.0 -> 16.6 ms at the same bars) but the c1
+// bench's uncentered byte covariances took 31-37 sweeps instead of 28-29 (c1 8.06 ->
+// 7.0 M samples/s: the dominant direction holds an early filter to degree 1), and 0.5
+// stalled two k > 128 block-locking cases above the accept floor.
 struct ChebPlan {
   int m = 0;
   double cc = 0, e = 1, s1 = 0;

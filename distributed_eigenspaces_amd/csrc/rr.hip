@@ -825,6 +825,7 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
     }
     for (int st = 0; st < p - 1; ++st) {
       const int ci = 1 + (st & 1);
+#ifdef DEIG_AB_RR_JOLD
       if (tid < half) {
         int a, b;
         if (tid == 0) {
@@ -842,6 +843,32 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
         }
         rotp[tid] = f32x4{c, s, __int_as_float(a), __int_as_float(b)};
       }
+#else
+      // the p / 2 <= 64 pairs of a step are one wave's lanes: the step's rotation count
+      // is a ballot (64 LDS atomics on one address serialised ~0.2 us per step)
+      if (wave == 0) {
+        bool rot = false;
+        if (tid < half) {
+          int a, b;
+          if (tid == 0) {
+            a = p - 1;
+            b = st;
+          } else {
+            a = (st + tid) % (p - 1);
+            b = (st - tid + (p - 1)) % (p - 1);
+          }
+          const float app = X1[a * p + a], aqq = X1[b * p + b], apq = X1[a * p + b];
+          float c = 1.f, s = 0.f;
+          if (fabsf(apq) > abs_thr && fabsf(apq) > jrel * __builtin_amdgcn_sqrtf(fabsf(app * aqq))) {
+            rr_rot_cs(app, aqq, apq, c, s);
+            rot = true;
+          }
+          rotp[tid] = f32x4{c, s, __int_as_float(a), __int_as_float(b)};
+        }
+        const int cnt = __popcll(__ballot(rot));
+        if (tid == 0) nrot[ci] = cnt;
+      }
+#endif
       __syncthreads();
       const int step_rot = nrot[ci];
       if (step_rot != 0) {

@@ -1,0 +1,77 @@
+"""Solver schedule A/B through deig_solver_opts (no rebuild): for the worker shapes of
+c1 / c3 / c5, time topk_eigh under several option sets (median of reps, one process)
+and check each result against the float64 eigendecomposition of the same S (‖P - P_ref‖_F,
+eigenvalues) - the bars are the parity bars (1e-4 / 1e-5).  Measurement tooling.
+
+  python tools/solver_opts_sweep.py [--reps R] [--cases c5,c3]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+VARIANTS = {
+    "default": {},
+    "cheb_0.1": {"cheb_above": 0.1},
+    "cheb_0.3": {"cheb_above": 0.3},
+    "cheb_0.5": {"cheb_above": 0.5},
+    "cheb_1.0": {"cheb_above": 1.0},
+    "cheb_all": {"cheb_above": 10.0},
+    "rr3": {"rr_every": 3},
+    "jcap1": {"jacobi_early_sweeps": 1},
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--cases", default="c5,c3,c1")
+    a = ap.parse_args()
+    import torch
+    import distributed_eigenspaces_amd as de
+    from distributed_eigenspaces_amd import _lib, synthetic
+    dev = torch.device("cuda", 0)
+    shapes = {"c1": (6250, 3072, 10), "c3": (16384, 8192, 64), "c5": (32768, 16384, 128),
+              "c5n": (65536, 16384, 128), "c2": (1 << 20, 3072, 16)}
+    for name in a.cases.split(","):
+        n, d, k = shapes[name]
+        U = synthetic.planted_basis(d, k, seed=0, device=dev)
+        X = synthetic.spiked_samples(n, U, seed=1)
+        S = de.sigma_hat(X)
+        del X
+        # float64 reference top-k of the same S (fp64 eigh on the device)
+        w, V = torch.linalg.eigh(S.double())
+        wr, Vr_ = w[-k:].flip(0), V[:, -k:].flip(1)
+        Pr = Vr_ @ Vr_.t() if d <= 8192 else None
+        del w, V
+        torch.cuda.synchronize()
+        for vname, fields in VARIANTS.items():
+            o = _lib.solver_opts(**fields)
+            ts, r = [], None
+            for _ in range(a.reps):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                r = de.topk_eigh(S, k, check_finite=False, opts=o)
+                torch.cuda.synchronize()
+                ts.append((time.perf_counter() - t0) * 1e3)
+            Vg = r.V.double()
+            if Pr is not None:
+                pd = float(torch.linalg.matrix_norm(Vg @ Vg.t() - Pr))
+            else:
+                sv = torch.linalg.svdvals(Vg.t() @ Vr_).clamp(max=1)
+                pd = float(((1 - sv.pow(2)).clamp(min=0).sum() * 2).sqrt())
+            ev = float(((r.evals.double().flip(0) - wr).abs() / wr.abs()).max())
+            print(json.dumps({"case": name, "variant": vname, "ms": round(statistics.median(ts), 3),
+                              "sweeps": r.sweeps, "resid": r.resid, "converged": r.converged,
+                              "P_dist": pd, "eval_rel": ev}), flush=True)
+        del S, Vr_, Pr
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
