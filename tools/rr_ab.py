@@ -4,7 +4,7 @@ against the r03 rr_small_body (-DDEIG_AB_RR_V1), in ONE process on the same matr
 Measurement tooling only (the shipped library has no knobs).
 
   python tools/rr_ab.py build            # here: tools/ab_libs/libdeig_rrv1.so
-  python tools/rr_ab.py run [--reps R]   # GPU box: per case solve ms (median), sweeps,
+  python tools/rr_ab.py run [--reps R] [--other LIB]   # GPU box: per case solve ms (median), sweeps,
                                          # residual and the two solves' agreement
 (rocprofv3 --kernel-trace --stats around `run` gives rr_small_kernel vs
 rr_small2_kernel averages.)
@@ -55,13 +55,13 @@ def _bind(path):
     return L
 
 
-def run(reps):
+def run(reps, other=None):
     import torch
 
     import distributed_eigenspaces_amd as de
     from distributed_eigenspaces_amd import _lib, synthetic
     dev = torch.device("cuda", 0)
-    libs = {"v2": _bind(_lib.LIB_PATH), "v1": _bind(V1)}
+    libs = {"v2": _bind(_lib.LIB_PATH), "v1": _bind(other or V1)}
     cases = [("c1", 6250, 3072, 10), ("c2", 1 << 16, 3072, 16), ("c3", 16384, 8192, 64),
              ("c5", 32768, 16384, 128)]
     for name, n, d, k in cases:
@@ -100,8 +100,9 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("cmd", choices=["build", "run"])
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--other", default=None, help="B library for run (default: the r03 solve)")
     a = ap.parse_args()
     if a.cmd == "build":
         build()
     else:
-        run(a.reps)
+        run(a.reps, a.other)

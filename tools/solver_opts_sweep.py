@@ -17,13 +17,11 @@ sys.path.insert(0, ROOT)
 
 VARIANTS = {
     "default": {},
-    "cheb_0.1": {"cheb_above": 0.1},
-    "cheb_0.3": {"cheb_above": 0.3},
-    "cheb_0.5": {"cheb_above": 0.5},
-    "cheb_1.0": {"cheb_above": 1.0},
-    "cheb_all": {"cheb_above": 10.0},
     "rr3": {"rr_every": 3},
     "jcap1": {"jacobi_early_sweeps": 1},
+    "jcap3": {"jacobi_early_sweeps": 3},
+    "jcap0": {"jacobi_early_sweeps": 0},
+    "jabove1e-3": {"jacobi_early_above": 1e-3},
 }
 
 
