@@ -17,11 +17,11 @@ sys.path.insert(0, ROOT)
 
 VARIANTS = {
     "default": {},
-    "rr3": {"rr_every": 3},
-    "jcap1": {"jacobi_early_sweeps": 1},
-    "jcap3": {"jacobi_early_sweeps": 3},
-    "jcap0": {"jacobi_early_sweeps": 0},
-    "jabove1e-3": {"jacobi_early_above": 1e-3},
+    "fast3e-4": {"fast_until": 3e-4},
+    "fast1e-4": {"fast_until": 1e-4},
+    "fast1e-4_round1e-5": {"fast_until": 1e-4, "round_until": 1e-5},
+    "fast3e-5_round3e-6": {"fast_until": 3e-5, "round_until": 3e-6},
+    "round1e-5": {"round_until": 1e-5},
 }
 
 
