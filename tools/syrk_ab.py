@@ -42,10 +42,10 @@ def main():
     X = synthetic.spiked_samples(a.n, U, seed=1)
     st = torch.cuda.current_stream(dev)
     code = _lib.DEIG_SYRK_SPLIT3
-    wss = []
-    for L in libs:
-        nb = L.deig_syrk_workspace_ex(a.n, a.d, code)
-        wss.append((torch.empty(nb, dtype=torch.uint8, device=dev), nb))
+    # one workspace of the largest size for every library (each gets its own size)
+    sizes = [L.deig_syrk_workspace_ex(a.n, a.d, code) for L in libs]
+    big = torch.empty(max(sizes), dtype=torch.uint8, device=dev)
+    wss = [(big, nb) for nb in sizes]
     outs = [torch.empty(a.d, a.d, device=dev) for _ in libs]
     times = [[] for _ in libs]
     for rep in range(a.reps + 1):
