@@ -651,7 +651,7 @@ def run_oneshot(args, cfg, world, rank, dev):
                                              "pixel-sum digits" if planes == 3 else "") + ")")
     elif algo == "split3":
         mfma_flops, peak = 3.0 * flops, BF16_MFMA_PEAK
-        kernel = ("covariance split3 (split_kernel + syrks_q_kernel + syrks_reduce_kernel + "
+        kernel = ("covariance split3 (split_kernel + syrks_h_kernel + syrks_reduce_kernel + "
                   "diag_corr_kernel)" if d > 4096 else
                   "covariance split3, fused split (syrks_kernel<..., true> + syrks_reduce_kernel + "
                   "diag_corr_kernel)")

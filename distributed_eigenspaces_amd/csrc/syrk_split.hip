@@ -975,6 +975,203 @@ __device__ __forceinline__ void segment_q(const SSched& s, unsigned char* lds, i
   }
 }
 
+// ------------------------------------------------ half-refill ring (variant 30000)
+// The staggered kernel's two phases per K-tile (variant 12100: 48-MFMA M parts, half
+// the barriers of four phases) on segment_q's ring: phase h reads A quarters 2h and
+// 2h + 1 (and B in phase 0), and each region is restaged with K-tile t + 2 as soon as
+// both wave groups have read it.  Per wave and K-tile 8 pieces in two L parts of 4:
+//   L_0(t): B(t+1) parts 2, 3 and A quarters 2, 3 of t+1 into nxt (their previous
+//           contents, K-tile t-1's B and second half, were read by both groups by
+//           the barrier that opened this part);
+//   L_1(t): B(t+2) parts 0, 1 and A quarters 0, 1 of t+2 into cur (read in L_0(t)).
+// So every piece has ~1.5 K-tiles of lead instead of one.  RAW: a wave waits for its
+// own pieces of a region at the end of the L part before the one that reads it:
+// end of L_0(t) for A quarters 2, 3 of t (younger: L_1(t-1)'s 4 + L_0(t)'s 4 = 8);
+// end of L_1(t) for K-tile t+1's B and quarters 0, 1 (younger than its last piece,
+// B part 3 issued in L_0(t): quarters 2, 3 of t+1 + L_1(t)'s 4 = 6).  Near the end of
+// the segment the counts shrink with the pieces not issued.  WAR: every L part
+// retires its reads (lgkmcnt(0)) before its closing barrier.  Same MFMA order per
+// accumulator as the other variants (bit-identical sums).
+template <int PRIO>
+__device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, int tile, int64_t k0,
+                                          int64_t k1, int slot, bool partial, int pace_j) {
+  constexpr int BUF_B = Geo<2>::BUF_B;
+  constexpr int QB = 8 * 1024;  // one A quarter
+  constexpr int BOFF = 4 * QB;  // the B panel
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wi = wave >> 2, wj = wave & 3;
+  const bool lag = wave >= 4;
+  const int tt = __builtin_amdgcn_readfirstlane(s.order[tile]);
+  const int ti = tt & 0xffff, tj = tt >> 16;
+  const int i0 = ti * BT, j0 = tj * BT;
+  const bool diag = (ti == tj);
+  Acc<16> acc;
+  acc.zero();
+  float* slab = partial ? s.part + (int64_t)slot * SLAB : s.accs + (int64_t)blockIdx.x * SLAB;
+  bool flushed = false;
+  const int64_t nkt = k1 - k0;
+  auto bar = [&]() {  // raw barrier; nothing moves across it
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+  };
+  const int a_off = ti * BLOCK_B + wave * SLICE_B + ((lane >> 5) * 128 + (lane & 31)) * 16;
+  const int b_off = tj * BLOCK_B + wave * SLICE_B + lane * 16;
+  const uint32_t nrec = (uint32_t)(s.nt * BLOCK_B);
+  auto ring_rsrc = [&](int64_t kt) {
+    return make_rsrc(s.XP + kt * (int64_t)s.nt * BLOCK_B, nrec);
+  };
+  auto issue_a = [&](int64_t kt, int q, unsigned char* buf) {
+    const i32x4 r = ring_rsrc(kt);
+    int o = a_off + q * 512;
+    asm volatile("" : "+v"(o));
+    dma16(r, o, buf + q * QB + wave * 1024);
+  };
+  auto issue_b = [&](int64_t kt, unsigned char* buf, int p0, int p1) {
+    const i32x4 r = ring_rsrc(kt);
+    int o = b_off;
+    asm volatile("" : "+v"(o));
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      if (p >= p0 && p < p1) dma16(r, o + p * 1024, buf + BOFF + wave * SLICE_B + p * 1024);
+  };
+  if (nkt > 0) {
+    wait_vm<0>();     // the previous segment's stores / flushes
+    __syncthreads();  // ... and its last reads of the ring
+    // K-tile k0 whole, then K-tile k0 + 1's B parts 0, 1 and quarters 0, 1 (as an
+    // L_1 of K-tile k0 - 1 would have issued them)
+    issue_b(k0, lds, 0, 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) issue_a(k0, q, lds);
+    if (nkt > 1) {
+      issue_b(k0 + 1, lds + BUF_B, 0, 2);
+      issue_a(k0 + 1, 0, lds + BUF_B);
+      issue_a(k0 + 1, 1, lds + BUF_B);
+      wait_vm<4>();  // K-tile k0 landed
+    } else {
+      wait_vm<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    if (lag) bar();  // the stagger
+    const int c = lane & 15, g4 = lane >> 4;
+    int since = 0, since_pace = 0;
+    const int xcd = blockIdx.x & 7;
+    const unsigned nx = (unsigned)((s.G >> 3) + (xcd < (s.G & 7) ? 1 : 0));
+    bf16x8 bhi[4], blo[4];
+    bf16x8 ahi[4], alo[4];
+    for (int64_t t = 0; t < nkt; ++t) {
+      unsigned char* cur = lds + (t & 1) * BUF_B;
+      unsigned char* nxt = lds + ((t + 1) & 1) * BUF_B;
+      const bool has1 = t + 1 < nkt, has2 = t + 2 < nkt;
+      const unsigned char* pa = cur + ((g4 * 2) * 64 + 32 * wi + c) * 16;
+      const unsigned char* pb = cur + BOFF + ((g4 * 2) * BT + 64 * wj + c) * 16;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        // ---------------- L part
+        if (h == 0) {
+          if (pace_j >= 0 && ++since_pace == s.pace_kt) {
+            since_pace = 0;
+            ++pace_j;
+            if (threadIdx.x == 0) xcd_pace(s.pace + 32 * xcd, (unsigned)pace_j * nx);
+          }
+          if (since == s.flush_kt) {
+            flush<16>(slab, !flushed, acc, wave, lane);
+            wait_vm<0>();
+            flushed = true;
+            since = 0;
+          }
+          ++since;
+          if (has1) {
+            issue_b(k0 + t + 1, nxt, 2, 4);
+            issue_a(k0 + t + 1, 2, nxt);
+            issue_a(k0 + t + 1, 3, nxt);
+          }
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb) {
+            bhi[nb] = *reinterpret_cast<const bf16x8*>(pb + (16 * nb) * 16);
+            blo[nb] = *reinterpret_cast<const bf16x8*>(pb + (BT + 16 * nb) * 16);
+          }
+        } else if (has2) {
+          issue_b(k0 + t + 2, cur, 0, 2);
+          issue_a(k0 + t + 2, 0, cur);
+          issue_a(k0 + t + 2, 1, cur);
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int q = 2 * h + (m >> 1), mm = m & 1;
+          ahi[m] = *reinterpret_cast<const bf16x8*>(pa + q * QB + (16 * mm) * 16);
+          alo[m] = *reinterpret_cast<const bf16x8*>(pa + q * QB + (64 + 16 * mm) * 16);
+        }
+        if (h == 0) {
+          if (has1) wait_vm<8>(); else wait_vm<0>();
+        } else {
+          if (has2) wait_vm<6>(); else if (has1) wait_vm<2>(); else wait_vm<0>();
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        bar();
+        // ---------------- M part
+        if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int mb = 4 * h + m;
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb)
+            acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[m], bhi[nb], acc.a[mb][nb], 0, 0, 0);
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb)
+            acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[m], blo[nb], acc.a[mb][nb], 0, 0, 0);
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb)
+            acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[m], bhi[nb], acc.a[mb][nb], 0, 0, 0);
+        }
+        if (PRIO) __builtin_amdgcn_s_setprio(0);
+        bar();
+      }
+    }
+    if (!lag) bar();  // balance the stagger
+  }
+  if (flushed) unflush<16>(slab, acc, wave, lane);
+  if (partial) {
+#pragma unroll
+    for (int q = 0; q < NQUAD; ++q)
+      *slab_at(slab, wave, q, lane) = f32x4{acc.at(q, 0), acc.at(q, 1), acc.at(q, 2), acc.at(q, 3)};
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < NQUAD; ++q) {
+    const float a[4] = {acc.at(q, 0), acc.at(q, 1), acc.at(q, 2), acc.at(q, 3)};
+    store4(s, i0 + 128 * wi + Acc<16>::qrow(q, lane), j0 + 64 * wj + Acc<16>::qcol(q, lane), diag, a);
+  }
+}
+
+template <int PRIO>
+__global__ __launch_bounds__(NTHR) void syrks_h_kernel(SSched s) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * Geo<2>::BUF_B];
+  const int L = xcd_logical(blockIdx.x, s.G);
+  const int items = s.R * s.nseg;
+  const int nwork = s.q + (L < items ? (items - 1 - L) / s.G + 1 : 0);
+  for (int w = 0; w < nwork; ++w) {
+    int tile, slot = 0;
+    int64_t k0 = 0, k1 = s.NK;
+    const bool partial = w >= s.q;
+    if (!partial) {
+      tile = w * s.G + L;
+    } else {
+      const int i = L + (w - s.q) * s.G;
+      const int sg = i / s.R, r = i - sg * s.R;
+      tile = s.q * s.G + r;
+      slot = i;
+      k0 = __builtin_amdgcn_readfirstlane((int)(s.NK * sg / s.nseg));
+      k1 = __builtin_amdgcn_readfirstlane((int)(s.NK * (sg + 1) / s.nseg));
+    }
+    const int pace_j = (!partial && s.pace_kt > 0) ? (int)(w * (s.NK / s.pace_kt)) : -1;
+    segment_h<PRIO>(s, lds, tile, k0, k1, slot, partial, pace_j);
+  }
+}
+
 template <int PRIO, int KO, int DS>
 __global__ __launch_bounds__(NTHR) void syrks_q_kernel(SSched s) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[2 * Geo<2>::BUF_B];
@@ -1210,15 +1407,22 @@ int64_t default_chunk_rows(int64_t n, int64_t d) {
 // A/B builds (tools/, never the shipped library) fix one with -DDEIG_AB_SYRK_VARIANT=N.
 // Staggered-phase variants are 1PQR0: P phases per K-tile, the next K-tile's
 // pieces over Q of them, R = 1: s_setprio(1) around the MFMA clusters; 20DR0: the
-// quarter-refill ring (segment_q) with DMA schedule D.  Default 20100 (config-3 shard,
-// interleaved A/B in one process, bit-identical: 20000 315.3 vs 14200 319.6 ms,
-// profiles/r03f_syrk_qring_insplit_ab.log; 20100 318.5 vs 20000 323.7 ms on another
-// box, profiles/r03l_syrk_dma_schedule_ab.log); + 100000 * KO adds the knock-outs
-// (measurement builds only).
+// quarter-refill ring (segment_q) with DMA schedule D; 30000: the two-phase half-
+// refill ring (segment_h).  Default 30000 since r04 (config-3 shard, interleaved A/B in
+// one process, bit-identical, two orders on one box: 310.6 / 312.6 ms against 316.2 /
+// 319.3 for two staggered phases 12100 and 322.3 / 322.0 for the r03 default 20100,
+// profiles/r04w_syrk_half_ring_ab*.log): two phases halve the barriers per K-tile and
+// their 48-MFMA M parts cover the L parts' DMA issue (12100 alone: 311.0 vs 318.0 ms
+// for 20100 on another box; four phases 14100 / 14300 350 / 331, eight 360-366 ms,
+// s_setprio 12110 323.5, profiles/r04t_*, r04u_*), and the half ring gives every piece
+// ~1.5 K-tiles of lead instead of one.  History: r03 20000 315.3 vs 14200 319.6 ms,
+// profiles/r03f_syrk_qring_insplit_ab.log; 20100 318.5 vs 20000 323.7 ms,
+// profiles/r03l_syrk_dma_schedule_ab.log.  + 100000 * KO adds the knock-outs
+// (measurement builds only; the half ring has none).
 #ifdef DEIG_AB_SYRK_VARIANT
 constexpr int kSyrkLarge = DEIG_AB_SYRK_VARIANT;
 #else
-constexpr int kSyrkLarge = 20100;
+constexpr int kSyrkLarge = 30000;
 #endif
 int syrk_variant(int64_t d) {
 #ifdef DEIG_AB_SYRK_VARIANT
@@ -1232,7 +1436,9 @@ int syrk_variant(int64_t d) {
 // The split-pass kernel of variant V (instantiated for kSyrkLarge only).
 template <int V>
 void launch_split_pass_kernel(int G, hipStream_t stream, const SSched& s) {
-  if constexpr (V % 100000 >= 20000) {
+  if constexpr (V % 100000 >= 30000) {
+    hipLaunchKernelGGL((syrks_h_kernel<(V / 10) % 10>), dim3(G), dim3(NTHR), 0, stream, s);
+  } else if constexpr (V % 100000 >= 20000) {
     hipLaunchKernelGGL((syrks_q_kernel<(V / 10) % 10, V / 100000, (V / 100) % 10>), dim3(G), dim3(NTHR), 0,
                        stream, s);
   } else if constexpr (V >= 10000) {

@@ -30,7 +30,7 @@ def source_sha256():
                   "rb").read())
     return h.hexdigest()
 
-KERNELS = ["split_kernel", "syrks_kernel", "syrks_st_kernel", "syrks_q_kernel", "syrks_reduce_kernel", "diag_corr_kernel",
+KERNELS = ["split_kernel", "syrks_kernel", "syrks_st_kernel", "syrks_q_kernel", "syrks_h_kernel", "syrks_reduce_kernel", "diag_corr_kernel",
            "tile_order_kernel", "syrk_kernel", "syrk_reduce_kernel"]
 PAT = re.compile(r"\b(" + "|".join(KERNELS) + r")\b")
 
