@@ -652,7 +652,7 @@ def run_oneshot(args, cfg, world, rank, dev):
     elif algo == "split3":
         mfma_flops, peak = 3.0 * flops, BF16_MFMA_PEAK
         kernel = ("covariance split3 (split_kernel + syrks_h_kernel + syrks_reduce_kernel + "
-                  "diag_corr_kernel)" if d > 4096 else
+                  "diag_corr_kernel)" if d > 2048 else
                   "covariance split3, fused split (syrks_kernel<..., true> + syrks_reduce_kernel + "
                   "diag_corr_kernel)")
         algorithmic = (f"3 * n*d*(d+1) = {3 * flops:.4e} bf16 MFMA flop per launch (n = {ni} rows; "

@@ -84,6 +84,8 @@ struct SSched {
   int prio;      // 1: waves 4-7 run at s_setprio 1 (the arbitration losers otherwise)
   unsigned* pace;  // per-XCD arrival counters (128 B apart), zeroed per launch
   int pace_kt;     // K-tiles between two XCD pacing points (0: off)
+  int xm;          // remainder: segments per XCD, XCD-major numbering (0: global)
+  int rpace;       // remainder rounds paced too (segment_h only)
   // fused split (variant 163): X is staged as fp32 and split in LDS
   const float* X;
   int64_t ldx, nrows;
@@ -975,6 +977,54 @@ __device__ __forceinline__ void segment_q(const SSched& s, unsigned char* lds, i
   }
 }
 
+// Pacing points of one segment: point j (1..n) waits for the XCD counter to reach
+// base + j * mult (n = 0: none).
+struct PaceSeq {
+  int n;
+  unsigned base, mult;
+};
+
+// Blocks of this block's XCD (logical L) that run a remainder item in round u.
+// Global numbering: item i = L + u G (the XCD's blocks are logical [L - b/8, + nx));
+// XCD-major (s.xm > 0, G % 8 == 0): XCD x owns segments [x xm, (x + 1) xm) and its
+// G / 8 blocks take their items j = l + u G / 8 (j = local segment * R + r).
+__device__ __forceinline__ int rem_active(const SSched& s, int L, int u) {
+  if (s.xm) {
+    const int gx = s.G >> 3, left = s.R * s.xm - u * gx;
+    return left < 0 ? 0 : (left < gx ? left : gx);
+  }
+  const int xcd = blockIdx.x & 7;
+  const int nx = (s.G >> 3) + (xcd < (s.G & 7) ? 1 : 0);
+  const int left = s.R * s.nseg - u * s.G - (L - (int)(blockIdx.x >> 3));
+  return left < 0 ? 0 : (left < nx ? left : nx);
+}
+
+__device__ __forceinline__ int rem_rounds(const SSched& s, int L) {
+  if (s.xm) {
+    const int gx = s.G >> 3, l = L % gx, items = s.R * s.xm;
+    return l < items ? (items - 1 - l) / gx + 1 : 0;
+  }
+  const int items = s.R * s.nseg;
+  return L < items ? (items - 1 - L) / s.G + 1 : 0;
+}
+
+// Round u's item of block L: tile index, slot (= segment * R + r) and segment.
+__device__ __forceinline__ void rem_item(const SSched& s, int L, int u, int& tile, int& slot, int& sg) {
+  int r;
+  if (s.xm) {
+    const int gx = s.G >> 3, x = L / gx, j = L - x * gx + u * gx;
+    const int sl = j / s.R;
+    r = j - sl * s.R;
+    sg = x * s.xm + sl;
+  } else {
+    const int i = L + u * s.G;
+    sg = i / s.R;
+    r = i - sg * s.R;
+  }
+  tile = s.q * s.G + r;
+  slot = sg * s.R + r;
+}
+
 // ------------------------------------------------ half-refill ring (variant 30000)
 // The staggered kernel's two phases per K-tile (variant 12100: 48-MFMA M parts, half
 // the barriers of four phases) on segment_q's ring: phase h reads A quarters 2h and
@@ -994,7 +1044,7 @@ __device__ __forceinline__ void segment_q(const SSched& s, unsigned char* lds, i
 // accumulator as the other variants (bit-identical sums).
 template <int PRIO>
 __device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, int tile, int64_t k0,
-                                          int64_t k1, int slot, bool partial, int pace_j) {
+                                          int64_t k1, int slot, bool partial, const PaceSeq& pc) {
   constexpr int BUF_B = Geo<2>::BUF_B;
   constexpr int QB = 8 * 1024;  // one A quarter
   constexpr int BOFF = 4 * QB;  // the B panel
@@ -1057,9 +1107,9 @@ __device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, i
     bar();
     if (lag) bar();  // the stagger
     const int c = lane & 15, g4 = lane >> 4;
-    int since = 0, since_pace = 0;
+    int since = 0, since_pace = 0, pace_left = pc.n;
+    unsigned pace_t = pc.base;
     const int xcd = blockIdx.x & 7;
-    const unsigned nx = (unsigned)((s.G >> 3) + (xcd < (s.G & 7) ? 1 : 0));
     bf16x8 bhi[4], blo[4];
     bf16x8 ahi[4], alo[4];
     for (int64_t t = 0; t < nkt; ++t) {
@@ -1072,10 +1122,11 @@ __device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, i
       for (int h = 0; h < 2; ++h) {
         // ---------------- L part
         if (h == 0) {
-          if (pace_j >= 0 && ++since_pace == s.pace_kt) {
+          if (pace_left > 0 && ++since_pace == s.pace_kt) {
             since_pace = 0;
-            ++pace_j;
-            if (threadIdx.x == 0) xcd_pace(s.pace + 32 * xcd, (unsigned)pace_j * nx);
+            --pace_left;
+            pace_t += pc.mult;
+            if (threadIdx.x == 0) xcd_pace(s.pace + 32 * xcd, pace_t);
           }
           if (since == s.flush_kt) {
             flush<16>(slab, !flushed, acc, wave, lane);
@@ -1151,24 +1202,34 @@ template <int PRIO>
 __global__ __launch_bounds__(NTHR) void syrks_h_kernel(SSched s) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[2 * Geo<2>::BUF_B];
   const int L = xcd_logical(blockIdx.x, s.G);
-  const int items = s.R * s.nseg;
-  const int nwork = s.q + (L < items ? (items - 1 - L) / s.G + 1 : 0);
+  const int nwork = s.q + rem_rounds(s, L);
+  const int xcd = blockIdx.x & 7;
+  const unsigned nx = (unsigned)((s.G >> 3) + (xcd < (s.G & 7) ? 1 : 0));
+  // Full phases: every block runs P = NK / pace_kt points per tile.  Remainder rounds
+  // (rpace): Pm points per item, Pm from the shortest segment, so every item of a
+  // round runs the same count and the targets stay exact across rounds.
+  const unsigned P = s.pace_kt > 0 ? (unsigned)(s.NK / s.pace_kt) : 0u;
+  const int Pm = (s.pace_kt > 0 && s.rpace && s.nseg > 0) ? (int)(s.NK / s.nseg / s.pace_kt) : 0;
+  unsigned rbase = (unsigned)s.q * P * nx;
   for (int w = 0; w < nwork; ++w) {
-    int tile, slot = 0;
+    int tile, slot = 0, sg = 0;
     int64_t k0 = 0, k1 = s.NK;
     const bool partial = w >= s.q;
+    PaceSeq pc{0, 0u, 0u};
     if (!partial) {
       tile = w * s.G + L;
+      pc = PaceSeq{(int)P, (unsigned)w * P * nx, nx};
     } else {
-      const int i = L + (w - s.q) * s.G;
-      const int sg = i / s.R, r = i - sg * s.R;
-      tile = s.q * s.G + r;
-      slot = i;
+      rem_item(s, L, w - s.q, tile, slot, sg);
       k0 = __builtin_amdgcn_readfirstlane((int)(s.NK * sg / s.nseg));
       k1 = __builtin_amdgcn_readfirstlane((int)(s.NK * (sg + 1) / s.nseg));
+      if (Pm > 0) {
+        unsigned before = 0;
+        for (int u = 0; u < w - s.q; ++u) before += (unsigned)rem_active(s, L, u);
+        pc = PaceSeq{Pm, rbase + before * (unsigned)Pm, (unsigned)rem_active(s, L, w - s.q)};
+      }
     }
-    const int pace_j = (!partial && s.pace_kt > 0) ? (int)(w * (s.NK / s.pace_kt)) : -1;
-    segment_h<PRIO>(s, lds, tile, k0, k1, slot, partial, pace_j);
+    segment_h<PRIO>(s, lds, tile, k0, k1, slot, partial, pc);
   }
 }
 
@@ -1268,6 +1329,10 @@ __device__ __forceinline__ uint32_t bf16_rne(float x) {
   return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
 }
 
+// (r04, measured and not kept: one 16-B load per lane and row, lane -> features
+// 4 lane + j, so each hi / lo store covers 16 B at a 64-B stride: config 2 op 27.54 vs
+// 25.74 ms, config-3 shard 315.3 vs 307.7, profiles/r04zb_syrk_*_ab.log - most likely
+// the stores: below, each wave store instruction writes 1 KiB contiguous.)
 // X rows [0, n) of the chunk -> XP (noct octets; rows >= n and features >= d
 // are zeros) + per-block partial sums of lo^2 per feature (corr[blockIdx.y][f]).
 // grid (dp / 256, YB), 256 threads; lane handles features fb + lane + 64 q.
@@ -1353,8 +1418,35 @@ int remainder_segments(int64_t R, int G) {
   return 1;
 }
 
+// Remainder schedule of the half-ring kernel: bit 0 paces remainder rounds, bit 1
+// numbers remainder items XCD-major.  Default 1 since r04 (interleaved A/B in one
+// process, profiles/r04za_syrk_*_ab.log, unpaced / paced / XCD-major / both): config 2
+// (d = 3072, all 78 tiles remainder) 26.84 / 26.13 / 27.15 / 26.34 ms; d = 4096 22.78 /
+// 22.45 / 23.37 / 22.58; d = 5120 71.8 / 66.7 / 72.6 / 66.1; config-3 shard 303.5 /
+// 305.0 / 305.0 / 304.1 (its 16 remainder tiles are 1/33 of the work; the XCD-major
+// build runs the same schedule there, so ~1.5 ms is the spread).  Unpaced, the blocks
+// of a remainder round drift apart over their ~2500 K-tiles as the full phases' did
+// (XCD pacing above); XCD-major numbering (each XCD's blocks on K ranges no other XCD
+// reads) costs more in balance (nseg a multiple of 8) than it saves in L2 misses.
+#ifdef DEIG_AB_SYRK_REM
+constexpr int kSyrkRem = DEIG_AB_SYRK_REM;
+#else
+constexpr int kSyrkRem = 1;
+#endif
+int syrk_variant(int64_t d);
+
+// XCD-major remainder: segments per XCD (<= 8) whose critical path
+// ceil(R xm / gx) / (8 xm) is within 2 % of the best.
+int xcd_segments(int64_t R, int gx) {
+  double best = 1e30;
+  for (int k = 1; k <= 8; ++k) best = fmin(best, (double)cdiv(R * k, gx) / (8 * k));
+  for (int k = 1; k <= 8; ++k)
+    if ((double)cdiv(R * k, gx) / (8 * k) <= best * 1.02) return k;
+  return 1;
+}
+
 struct Layout {
-  int64_t dp, nt, T, G, q, R, nseg, yb_max, chunk_rows;
+  int64_t dp, nt, T, G, q, R, nseg, xm, yb_max, chunk_rows;
   size_t off_order, off_pace, off_accs, off_part, off_corr, off_xp, total;
 };
 
@@ -1368,6 +1460,11 @@ Layout make_layout(int64_t n, int64_t d, int G, int64_t chunk_rows) {
   L.q = L.T / G;
   L.R = L.T % G;
   L.nseg = remainder_segments(L.R, G);
+  L.xm = 0;
+  if ((kSyrkRem & 2) && syrk_variant(d) % 100000 >= 30000 && G % 8 == 0 && L.R > 0) {
+    L.xm = xcd_segments(L.R, G / 8);
+    L.nseg = 8 * L.xm;
+  }
   L.yb_max = SPLIT_YB;
   L.chunk_rows = chunk_rows;
   size_t off = 0;
@@ -1419,6 +1516,11 @@ int64_t default_chunk_rows(int64_t n, int64_t d) {
 // profiles/r03f_syrk_qring_insplit_ab.log; 20100 318.5 vs 20000 323.7 ms,
 // profiles/r03l_syrk_dma_schedule_ab.log.  + 100000 * KO adds the knock-outs
 // (measurement builds only; the half ring has none).
+// The fused split up to d = 2048 since r04 (was 4096): with the half-refill ring the
+// split pass wins above (interleaved A/B, profiles/r04y_syrk_*_ab.log: config 2, d =
+// 3072, 26.9 vs 28.8 ms; d = 4096 22.7 vs 25.3; d = 2048 26.10 vs 26.09 - a tie, and
+// the fused path needs no image of the shard in the workspace).
+constexpr int64_t kFusedMaxD = 2048;
 #ifdef DEIG_AB_SYRK_VARIANT
 constexpr int kSyrkLarge = DEIG_AB_SYRK_VARIANT;
 #else
@@ -1429,7 +1531,7 @@ int syrk_variant(int64_t d) {
   (void)d;
   return DEIG_AB_SYRK_VARIANT;
 #else
-  return d <= 4096 ? 163 : kSyrkLarge;
+  return d <= kFusedMaxD ? 163 : kSyrkLarge;
 #endif
 }
 
@@ -1520,6 +1622,8 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
 #else
   s.pace_kt = 64;
 #endif
+  s.xm = (int)L.xm;
+  s.rpace = kSyrkRem & 1;
   hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(64), 0, stream, s.nt,
                      reinterpret_cast<int*>(base + L.off_order));
   DEIG_HIP_CHECK(hipGetLastError());
@@ -1528,7 +1632,7 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
   s.nrows = n;
   s.corr = corr;
   if (fused) {
-    DEIG_REQUIRE(ldx <= (int64_t(1) << 25), "syrk: ldx > 2^25 is not supported for d <= 4096");
+    DEIG_REQUIRE(ldx <= (int64_t(1) << 25), "syrk: ldx > 2^25 is not supported for d <= 2048");
     // One pass over all n rows (no XP image, no chunks).  lo^2 partials:
     // [segment < max(1, nseg)][octet wave < 4][dp], zero where no diagonal tile wrote.
     const int64_t yb = 4 * (L.nseg > 1 ? L.nseg : 1);

@@ -90,12 +90,14 @@ def test_no_cpu_fallback():
 
 
 def test_workspace_fused_split_variant():
-    """d <= 4096 (config 2) uses the fused split, which stages X itself: no image of
-    the shard in the workspace; d > 4096 keeps the split pass and its image."""
+    """d <= 2048 uses the fused split, which stages X itself: no image of the shard in
+    the workspace; d > 2048 (config 2's 3072 since r04) runs the split pass and its
+    image."""
     L = _lib.lib()
-    n, d = 1 << 20, 3072
+    n, d = 1 << 20, 2048
     ws = L.deig_syrk_workspace_ex(n, d, _lib.DEIG_SYRK_SPLIT3)
     assert 0 < ws < n * d * 4 // 10  # slabs only (the image would be n * d * 4)
+    assert L.deig_syrk_workspace_ex(n, 3072, _lib.DEIG_SYRK_SPLIT3) >= n * 3072 * 4
     assert L.deig_syrk_workspace_ex(1 << 21, 8192, _lib.DEIG_SYRK_SPLIT3) >= (1 << 21) * 8192 * 4
 
 

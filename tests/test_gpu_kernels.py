@@ -317,10 +317,10 @@ def test_sym_power_fused_chain(d, p, mode, cuda):
         assert torch.equal(h + m, q)
 
 
-@pytest.mark.parametrize("d", [4096, 4100])
+@pytest.mark.parametrize("d", [2048, 2052, 4096])
 def test_syrk_split3_variant_boundary(d, cuda):
-    """Either side of the default's width switch (fused split up to d = 4096, the
-    split pass above), ragged n: both vs float64."""
+    """Either side of the default's width switch (fused split up to d = 2048, the
+    split pass above since r04), ragged n: both vs float64."""
     rng = np.random.default_rng(d)
     X = (rng.standard_normal((2085, d)) + 0.25).astype(np.float32)
     _syrk_check(X, cuda, rel=_split3_tol(2085), algo="split3")

@@ -88,11 +88,11 @@ def test_split_pass_chunk_loop(d, cuda):
     assert _syrk_raw(x, 1.0 / n, S, _lib.DEIG_SYRK_SPLIT3, ws, 4096) == _lib.DEIG_EWORKSPACE
 
 
-@pytest.mark.parametrize("d", [8192, 8000, 3072])
+@pytest.mark.parametrize("d", [8192, 8000, 3072, 2048])
 def test_accumulate_row_blocks(d, cuda):
     """Four ragged row blocks streamed through sigma_hat(..., accumulate=True) into
-    one S with alpha = 1 / n_total: the covariance of all rows (d = 3072 runs the
-    fused-split kernel with beta = 1, d > 4096 the split pass).  Variant 2: the first
+    one S with alpha = 1 / n_total: the covariance of all rows (d = 2048 runs the
+    fused-split kernel with beta = 1, d > 2048 the split pass).  Variant 2: the first
     block without accumulate overwrites whatever S held."""
     import distributed_eigenspaces_amd as de
     sizes = [1000, 1031, 997, 1043]
