@@ -848,12 +848,17 @@ def run_oja(args, cfg, world, rank, dev):
         "rows_per_gpu_per_step": agg * b,
         "parallelism": f"dp{world} (one Oja stream per GPU; RCCL all-gather + broadcast of "
                        f"bases every {agg} batches)"})
-    line["roofline"] = {"bound": "hbm", "kernel": "Oja steps (oja_nn_kernel Xb*V + oja_tn_kernel "
-                        "V += c Xb^T*T, bf16x3 split products; CholQR every 8 batches), whole op "
-                        "per batch",
+    resident = b == 4096 and d % 512 == 0 and d <= 3072 and k <= 32  # DEIG_OJA_AUTO's choice
+    kname = ("Oja steps (oja_blk_kernel: one launch per run of 8 batches, Xb held in registers "
+             "and read from HBM once per batch, Xb*V and Xb^T*T as bf16x3 split products, "
+             "in-launch hand-offs; CholQR every 8 batches), whole op per batch" if resident else
+             "Oja steps (oja_nn_kernel Xb*V + oja_tn_kernel V += c Xb^T*T, bf16x3 split "
+             "products; CholQR every 8 batches), whole op per batch")
+    line["roofline"] = {"bound": "hbm", "kernel": kname,
                         "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK, "traffic": None,
-                        "algorithmic": f"8*b*d = {byt:.4e} bytes per batch (Xb read twice)",
+                        "algorithmic": f"8*b*d = {byt:.4e} bytes per batch (the two products each "
+                                       "stream Xb; the resident path reads it from HBM once)",
                         "launch_ms": oja_ms}
     line["cpu_baseline"] = cpu
     line["breakdown"] = {"oja_ms_per_batch": oja_ms,

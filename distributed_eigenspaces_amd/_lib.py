@@ -40,6 +40,10 @@ DEIG_U8_GRAY3 = 1
 U8_MODES = {"raw": DEIG_U8_RAW, "gray": DEIG_U8_GRAY3}
 DEIG_F32 = 0
 DEIG_F64 = 1
+DEIG_OJA_AUTO = 0
+DEIG_OJA_TWO_PASS = 1
+DEIG_OJA_RESIDENT = 2
+OJA_ALGOS = {"auto": DEIG_OJA_AUTO, "two_pass": DEIG_OJA_TWO_PASS, "resident": DEIG_OJA_RESIDENT}
 
 
 class SolverOpts(ctypes.Structure):
@@ -123,6 +127,9 @@ SIGNATURES = {
     "deig_oja_steps_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_float,
                                           _fp, ctypes.c_int, _c_i64, ctypes.c_int, _vp, _c_sz,
                                           _vp]),
+    "deig_oja_steps_ex": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_float,
+                                         _fp, ctypes.c_int, _c_i64, ctypes.c_int, ctypes.c_int, _vp,
+                                         _c_sz, _vp]),
     "deig_sym_apply_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _fp, ctypes.c_int, _c_i64, _fp,
                                           _c_i64, ctypes.c_float, ctypes.c_int, _vp, _c_sz, _vp]),
     "deig_sym_power_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _fp, ctypes.c_int, _c_i64, _fp,

@@ -1565,13 +1565,20 @@ int deig_sym_apply_f32(const float* S, int64_t d, int64_t lds, const float* Q, i
 
 size_t deig_oja_workspace(int64_t b, int64_t d, int k) { return oja_workspace_bytes(b, d, k); }
 
-int deig_oja_steps_f32(const float* X, int64_t nb, int64_t b, int64_t d, int64_t ldx, float eta,
-                       float* V, int k, int64_t ldv, int orth_every, void* ws, size_t ws_bytes,
-                       void* stream) {
+int deig_oja_steps_ex(const float* X, int64_t nb, int64_t b, int64_t d, int64_t ldx, float eta,
+                      float* V, int k, int64_t ldv, int orth_every, int algo, void* ws,
+                      size_t ws_bytes, void* stream) {
   g_err[0] = 0;
   if (!X || !V || !aligned16(X)) return fail(DEIG_EINVAL, "oja: X must be 16-byte aligned");
   return oja_steps_launch(X, nb, b, d, ldx, eta, V, k, ldv, orth_every, ws, ws_bytes,
-                          (hipStream_t)stream);
+                          (hipStream_t)stream, algo);
+}
+
+int deig_oja_steps_f32(const float* X, int64_t nb, int64_t b, int64_t d, int64_t ldx, float eta,
+                       float* V, int k, int64_t ldv, int orth_every, void* ws, size_t ws_bytes,
+                       void* stream) {
+  return deig_oja_steps_ex(X, nb, b, d, ldx, eta, V, k, ldv, orth_every, DEIG_OJA_AUTO, ws,
+                           ws_bytes, stream);
 }
 
 int deig_oja_step_f32(const float* Xb, int64_t b, int64_t d, int64_t ldx, float eta, float* V,

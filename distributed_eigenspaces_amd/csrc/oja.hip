@@ -6,6 +6,8 @@
 // batch (oja_nn_kernel, oja_tn_kernel), bf16x3 split products, K split over the
 // waves of a block and summed in LDS (no slab passes); each pass writes the next
 // one's MFMA operand image (T's for TN, V's for the next batch's NN).
+#include <algorithm>
+
 #include "deig_internal.hpp"
 
 namespace deig {
@@ -21,14 +23,16 @@ __global__ __launch_bounds__(256) void col_to_rowpad(const float* __restrict__ V
   Vr[idx] = (j < k) ? V[r + (int64_t)j * ldv] : 0.f;
 }
 
+// (*err set: a v4 hand-off timed out - the basis is poisoned with NaN, never returned
+// silently wrong)
 __global__ __launch_bounds__(256) void rowpad_to_col(const float* __restrict__ Vr, int64_t d,
                                                      int k, int kp, float* __restrict__ V,
-                                                     int64_t ldv) {
+                                                     int64_t ldv, const unsigned* __restrict__ err) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= d * k) return;
   const int j = (int)(idx / d);
   const int64_t r = idx - (int64_t)j * d;
-  V[r + (int64_t)j * ldv] = Vr[r * kp + j];
+  V[r + (int64_t)j * ldv] = *err ? __builtin_nanf("") : Vr[r * kp + j];
 }
 
 // G (kp x kp, leading k x k used) = L L^T;  Rinv = L^-T (upper), zero-padded to kp.
@@ -455,15 +459,359 @@ __global__ __launch_bounds__(512) void oja_tn_kernel(const float* __restrict__ X
   }
 }
 
+// ---------------------------------------------------------------- v4: one launch
+// Block-resident Oja (config 4's shape: b = 4096, d = 512 c <= 3072, kp <= 32).  One
+// persistent launch runs a run of batches; 256 workgroups (one per CU, 8 waves) tile
+// the batch as a 16 x 16 grid of X blocks - workgroup (i, j) owns rows
+// R_i = [256 i, 256 i + 256) and features F_j = [FB j, FB j + FB), FB = d / 16 - and
+// keeps its block in registers (wave w: rows 32 w .. 32 w + 31 as MFMA A fragments,
+// 96 VGPRs at FB = 192), so Xb is read from HBM ONCE per batch (the two-pass v3
+// reads it twice) and the next batch's block is prefetched while the basis update
+// finishes.  Per batch, with V_j = V[F_j], T = Xb V:
+//   1. P_ij = X_ij V_j (256 x kp; V_j's image staged in LDS), written to ppart;
+//   A. row group i: all 16 P_i. partials written;
+//   2. T rows R_i[16 j .. +16) = sum_j' P_ij' (fixed order), written as the TN operand
+//      image (timg);
+//   B. row group i: T_i complete;
+//   3. Q_ij = X_ij^T T_i (FB x kp: the block transposed per wave through LDS, the
+//      8 waves' row-step partials summed in LDS in wave order), written to qpart;
+//   C. column group j: all 16 Q_.j partials written;
+//   4. (one wave) V[F_j] slice += c sum_i' Q_i'j (fixed order) and its image entries;
+//   D. column group j: V_j's image complete.
+// Hand-offs (MI355X_MICROARCH.md visibility table, first row): payloads stored
+// write-through (sc1) and drained (vmcnt(0), then the workgroup barrier), ONE lane adds
+// to the group's counter, ONE lane polls it (relaxed agent loads), the payload is
+// read with sc1 loads only.  Column group j lives on one XCD (its C / D hand-offs stay
+// in that L2); row groups span all eight.  Counters are zeroed per launch and every
+// spin is bounded (2 s): a timeout sets *err, every later wait returns at once, and
+// the final copy-out poisons V with NaN - a failure is loud, never a hang.
+constexpr int OB_G = 256, OB_NR = 16, OB_NF = 16, OB_RB = 256, OB_TS = 36;
+constexpr int OB_CNT_LINE = 32;  // one counter per 128-B line
+
+struct OjaBlk {
+  const float* X;  // first batch of the run
+  int64_t ldx;
+  int64_t b;
+  int d, kp, nbatch;
+  float coef;      // eta / b
+  float* V;        // row-padded d x kp, updated in place
+  u32x4* vimg;     // V's image (NN B operand)
+  u32x4* timg;     // T's image (TN B operand)
+  float* ppart;    // [16 j][b / 4][kp][4]
+  float* qpart;    // [16 i][d / 4][kp][4]
+  unsigned* cnt;   // [4 phases][16 groups] x OB_CNT_LINE
+  unsigned* err;
+  unsigned long long* trace;  // measurement builds only (DEIG_AB_OJA_TRACE)
+};
+// Measurement builds only (-DDEIG_AB_OJA_TRACE, tools/oja_trace.py): per block and batch
+// 16 wall_clock64 stamps at the phase boundaries, in a buffer after the workspace.
+#ifdef DEIG_AB_OJA_TRACE
+#define OB_STAMP(slot, cond) \
+  if (cond) a.trace[((int64_t)blockIdx.x * 64 + (bt & 63)) * 16 + (slot)] = wall_clock64()
+#else
+#define OB_STAMP(slot, cond)
+#endif
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ob_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+// 16-B write-through store / L1-bypassing load (aux 16 = sc1)
+__device__ __forceinline__ void ob_st(const __amdgpu_buffer_rsrc_t& r, uint32_t off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 16);
+}
+__device__ __forceinline__ u32x4 ob_ld(const __amdgpu_buffer_rsrc_t& r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);
+}
+__device__ __forceinline__ void ob_signal(unsigned* c) {
+  __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// One lane: wait until *c >= target (bounded; see above).
+__device__ __forceinline__ void ob_wait(unsigned* c, unsigned target, unsigned* err) {
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    if (wall_clock64() - t0 > 200000000ull) {
+      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+__device__ __forceinline__ void ob_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+template <int NB, int NKS>
+__global__ __launch_bounds__(512) void oja_blk_kernel(OjaBlk a) {
+  constexpr int KP = 16 * NB;
+  constexpr int FB = 32 * NKS;
+  constexpr int VL_N = NKS * NB * 2 * 64;  // u32x4 of V_j's image
+  constexpr int NFT = 2 * NKS;              // feature tiles of the block
+  // feature tiles per step-3 reduction chunk: the largest even divisor of NFT up to 6
+  constexpr int CH = NFT <= 6 ? NFT : NFT % 6 == 0 ? 6 : NFT % 4 == 0 ? 4 : 2;
+  static_assert(NFT % CH == 0 && CH % 2 == 0, "step-3 chunks are whole k-steps");
+  // red (step 3's cross-wave sums) and vl (step 1's V_j image) are never live together
+  __shared__ f32x4 red[8][CH][NB][64];
+  static_assert(sizeof(red) >= VL_N * sizeof(u32x4), "vl aliases red");
+  u32x4* vl = reinterpret_cast<u32x4*>(&red[0][0][0][0]);
+  __shared__ __attribute__((aligned(16))) float xt[8][32 * OB_TS];
+  __shared__ float tt[16][KP + 1];
+  __shared__ unsigned step3_done, step4_done;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int t = threadIdx.x;
+  // column group j on one XCD: blocks b, b + 8, ... (XCD b & 7) take j = 2 x + s / 16
+  const int x = blockIdx.x & 7, sl = blockIdx.x >> 3;
+  const int j = 2 * x + (sl >> 4), i = sl & 15;
+  const int R0 = OB_RB * i, F0 = FB * j;
+  const int64_t b = a.b;
+  const int d = a.d;
+  unsigned* cA = a.cnt + (0 * 16 + i) * OB_CNT_LINE;
+  unsigned* cB = a.cnt + (1 * 16 + i) * OB_CNT_LINE;
+  unsigned* cC = a.cnt + (2 * 16 + j) * OB_CNT_LINE;
+  unsigned* cD = a.cnt + (3 * 16 + j) * OB_CNT_LINE;
+  const __amdgpu_buffer_rsrc_t rv = ob_rsrc(a.vimg, (uint32_t)((d / 32) * NB * 2 * 64 * 16));
+  const __amdgpu_buffer_rsrc_t rt = ob_rsrc(a.timg, (uint32_t)((b / 32) * NB * 2 * 64 * 16));
+  const __amdgpu_buffer_rsrc_t rp = ob_rsrc(a.ppart, (uint32_t)(16 * b * KP * 4));
+  const __amdgpu_buffer_rsrc_t rq = ob_rsrc(a.qpart, (uint32_t)(16 * (int64_t)d * KP * 4));
+
+  // this wave's X: rows R0 + 32 w + 16 rt + (lane & 15), features F0 + 32 ks + 8 (lane >> 4) + 4 h
+  f32x4 xr[2][NKS][2];
+  auto load_x_ks = [&](int bt, int ks) {
+    const float* xb = a.X + (int64_t)bt * b * a.ldx;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const float* row = xb + (int64_t)(R0 + 32 * wave + 16 * r + (lane & 15)) * a.ldx + F0 + 8 * (lane >> 4);
+      xr[r][ks][0] = *reinterpret_cast<const f32x4*>(row + 32 * ks);
+      xr[r][ks][1] = *reinterpret_cast<const f32x4*>(row + 32 * ks + 4);
+    }
+  };
+  auto load_x = [&](int bt) {
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) load_x_ks(bt, ks);
+  };
+  load_x(0);
+  for (int bt = 0; bt < a.nbatch; ++bt) {
+    const unsigned target = 16u * (unsigned)(bt + 1);
+    const bool more = bt + 1 < a.nbatch;
+    // ---- V_j's image -> LDS (written by the previous batch's step 4, or before the launch)
+    for (int u = t; u < VL_N; u += 512)  // k-steps F0 / 32 .. are contiguous in the image
+      vl[u] = ob_ld(rv, (uint32_t)(((int64_t)(F0 / 32) * NB * 2 * 64 + u) * 16));
+    __syncthreads();
+    OB_STAMP(0, t == 0);
+    // ---- 1. P = X_ij V_j
+    {
+      f32x4 acc[2][NB];
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) acc[r][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          bf16x8 ahi, alo;
+          split8(xr[r][ks][0], xr[r][ks][1], ahi, alo);
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) {
+            const bf16x8 bhi = __builtin_bit_cast(bf16x8, vl[((ks * NB + nb) * 2 + 0) * 64 + lane]);
+            const bf16x8 blo = __builtin_bit_cast(bf16x8, vl[((ks * NB + nb) * 2 + 1) * 64 + lane]);
+            acc[r][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi, acc[r][nb], 0, 0, 0);
+            acc[r][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, blo, acc[r][nb], 0, 0, 0);
+            acc[r][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bhi, acc[r][nb], 0, 0, 0);
+          }
+        }
+      }
+      // rows 4 (lane >> 4) + e of the tile, column 16 nb + (lane & 15): [j][row / 4][col][4]
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          const int64_t rq = (R0 + 32 * wave + 16 * r) / 4 + (lane >> 4);
+          const int col = 16 * nb + (lane & 15);
+          ob_st(rp, (uint32_t)((((int64_t)j * (b / 4) + rq) * KP + col) * 16),
+                __builtin_bit_cast(u32x4, acc[r][nb]));
+        }
+    }
+    ob_drain();
+    __syncthreads();
+    OB_STAMP(1, t == 0);
+    if (t == 0) {
+      ob_signal(cA);
+      ob_wait(cA, target, a.err);
+    }
+    __syncthreads();
+    OB_STAMP(2, t == 0);
+    // ---- 2. T rows R0 + 16 j .. + 15 = sum_j' P_ij'
+    if (t < 4 * KP) {
+      const int rql = t / KP, col = t - rql * KP;
+      const int64_t rq = (R0 + 16 * j) / 4 + rql;
+      f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int jj = 0; jj < OB_NF; ++jj)
+        s += __builtin_bit_cast(f32x4, ob_ld(rp, (uint32_t)((((int64_t)jj * (b / 4) + rq) * KP + col) * 16)));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) tt[4 * rql + e][col] = s[e];
+    }
+    __syncthreads();
+    if (t < 2 * KP) {
+      const int gi = t / KP, col = t - gi * KP;
+      float v[8];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) v[jj] = tt[8 * gi + jj][col];
+      bf16x8 hi, lo;
+      split8(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, hi, lo);
+      const int r0 = R0 + 16 * j;
+      const int ln = (col & 15) + 16 * ((r0 & 31) / 8 + gi);
+      ob_st(rt, (uint32_t)(img_index(r0 / 32, col / 16, 0, ln, NB) * 16), __builtin_bit_cast(u32x4, hi));
+      ob_st(rt, (uint32_t)(img_index(r0 / 32, col / 16, 1, ln, NB) * 16), __builtin_bit_cast(u32x4, lo));
+    }
+    ob_drain();
+    __syncthreads();
+    OB_STAMP(3, t == 0);
+    if (t == 0) {
+      ob_signal(cB);
+      ob_wait(cB, target, a.err);
+    }
+    __syncthreads();
+    OB_STAMP(4, t == 0);
+    // ---- 3. Q_ij = X_ij^T T_i: wave w takes row step w (its own rows) for every
+    // feature tile; its T_i fragments straight to registers
+    {
+      bf16x8 th[NB], tlo[NB];
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        th[nb] = __builtin_bit_cast(bf16x8, ob_ld(rt, (uint32_t)(img_index(R0 / 32 + wave, nb, 0, lane, NB) * 16)));
+        tlo[nb] = __builtin_bit_cast(bf16x8, ob_ld(rt, (uint32_t)(img_index(R0 / 32 + wave, nb, 1, lane, NB) * 16)));
+      }
+      float* T = xt[wave];
+      if (t == 0) step3_done = step4_done = 0;  // arrival counters (barriers follow)
+      // CH feature tiles (CH / 2 k-steps) at a time: their products, then the 8 row
+      // steps' partials summed in wave order
+#pragma unroll
+      for (int c0 = 0; c0 < NFT; c0 += CH) {
+        f32x4 acc[CH][NB];
+#pragma unroll
+        for (int kc = 0; kc < CH / 2; ++kc) {
+          const int ks = c0 / 2 + kc;
+          // this wave's 32 rows x 32 features of k-step ks, transposed: T[f][row]
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                T[(8 * (lane >> 4) + 4 * h + e) * OB_TS + 16 * r + (lane & 15)] = xr[r][ks][h][e];
+          // waves 0-5: this k-step of the next batch's block streams from here on (its
+          // registers are free once staged); waves 6, 7 publish Q and run step 4
+          // first, and their drains would wait for it
+          if (wave < 6 && more) load_x_ks(bt + 1, ks);
+#pragma unroll
+          for (int f2 = 0; f2 < 2; ++f2) {
+            const f32x4 a0 = *reinterpret_cast<const f32x4*>(T + (16 * f2 + (lane & 15)) * OB_TS + 8 * (lane >> 4));
+            const f32x4 a1 = *reinterpret_cast<const f32x4*>(T + (16 * f2 + (lane & 15)) * OB_TS + 8 * (lane >> 4) + 4);
+            bf16x8 ahi, alo;
+            split8(a0, a1, ahi, alo);
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb) {
+              f32x4 c = {0.f, 0.f, 0.f, 0.f};
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, th[nb], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, tlo[nb], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, th[nb], c, 0, 0, 0);
+              acc[2 * kc + f2][nb] = c;
+            }
+          }
+        }
+#pragma unroll
+        for (int ft = 0; ft < CH; ++ft)
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) red[wave][ft][nb][lane] = acc[ft][nb];
+        __syncthreads();
+        for (int u = t - 384; u >= 0 && u < CH * NB * 64; u += 128) {  // waves 6, 7
+          const int ln = u & 63, nb = (u >> 6) % NB, ft = (u >> 6) / NB;
+          f32x4 sm = red[0][ft][nb][ln];
+#pragma unroll
+          for (int w = 1; w < 8; ++w) sm += red[w][ft][nb][ln];
+          const int64_t fq = (F0 + 16 * (c0 + ft)) / 4 + (ln >> 4);
+          const int col = 16 * nb + (ln & 15);
+          ob_st(rq, (uint32_t)((((int64_t)i * (d / 4) + fq) * KP + col) * 16), __builtin_bit_cast(u32x4, sm));
+        }
+        __syncthreads();
+      }
+    }
+    OB_STAMP(5, t == 0);
+    if (wave >= 6) {
+      // Q published by waves 6, 7 only: both drained, the second to arrive signals
+      ob_drain();
+      if (lane == 0 && atomicAdd(&step3_done, 1u) == 1u) ob_signal(cC);
+      // ---- 4. (waves 6, 7) V[F_j] group of 8 features g = i + 16 (wave - 6) (< FB / 8)
+      if (lane == 0) ob_wait(cC, target, a.err);
+      __builtin_amdgcn_wave_barrier();
+      OB_STAMP(6, lane == 0 && wave == 7);
+      const int col = lane >> 1, q = lane & 1;
+      const int g = i + OB_NR * (wave - 6);
+      if (g < FB / 8) {
+        f32x4 sm = {0.f, 0.f, 0.f, 0.f};
+        const int64_t fq = (F0 + 8 * g) / 4 + q;
+        if (col < KP) {
+#pragma unroll 4
+          for (int ii = 0; ii < OB_NR; ++ii)
+            sm += __builtin_bit_cast(f32x4, ob_ld(rq, (uint32_t)((((int64_t)ii * (d / 4) + fq) * KP + col) * 16)));
+        }
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t f = 4 * fq + e;
+          v[e] = 0.f;
+          if (col < KP) {
+            v[e] = fmaf(a.coef, sm[e], a.V[f * KP + col]);
+            a.V[f * KP + col] = v[e];
+          }
+        }
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = __shfl_xor(v[e], 1, 64);
+        // the group's 8 features in order: lane q = 0 holds 0..3, its partner 4..7
+        const f32x4 first = q ? f32x4{o[0], o[1], o[2], o[3]} : f32x4{v[0], v[1], v[2], v[3]};
+        const f32x4 second = q ? f32x4{v[0], v[1], v[2], v[3]} : f32x4{o[0], o[1], o[2], o[3]};
+        bf16x8 hh, ll;
+        split8(first, second, hh, ll);
+        if (col < KP) {
+          const int f8 = F0 + 8 * g;
+          const int ln = (col & 15) + 16 * ((f8 & 31) / 8);
+          ob_st(rv, (uint32_t)(img_index(f8 / 32, col / 16, q, ln, NB) * 16),
+                __builtin_bit_cast(u32x4, q ? ll : hh));
+        }
+      }
+      ob_drain();
+      OB_STAMP(7, lane == 0 && wave == 7);
+      if (lane == 0 && atomicAdd(&step4_done, 1u) == 1u) ob_signal(cD);
+      if (more) load_x(bt + 1);
+    }
+    OB_STAMP(8, t == 0);
+    if (more) {
+      if (t == 0) ob_wait(cD, target, a.err);
+      __syncthreads();
+    }
+    OB_STAMP(9, t == 0);
+  }
+}
+
 struct OjaWs {
+  unsigned *cnt, *err;  // v4 hand-off counters (zeroed per launch) and timeout word
   float *Vr, *Vr2, *G, *Rinv, *slab;
   u32x4 *vimg, *timg;  // bf16 operand images of V (NN) and T (TN)
+  float *ppart, *qpart;  // v4 partials
+  unsigned long long* trace;
   size_t slab_bytes;
 };
+constexpr size_t OB_CNT_BYTES = 4 * 16 * OB_CNT_LINE * sizeof(unsigned);
 
 OjaWs carve_oja(void* ws, size_t cap, int64_t b, int64_t d, int kp, size_t* total) {
   Carve c(ws, cap);
   OjaWs o;
+  // the counters first: the per-launch memset starts at the allocation and is a
+  // multiple of 16 B (cdna_hip_programming.md Guideline 16, Re-initialise every call)
+  o.cnt = c.take<unsigned>(OB_CNT_BYTES / sizeof(unsigned));
+  o.err = c.take<unsigned>(OB_CNT_LINE);
   o.Vr = c.take<float>((size_t)d * kp);
   o.Vr2 = c.take<float>((size_t)d * kp);
   o.G = c.take<float>((size_t)kp * kp);
@@ -476,6 +824,13 @@ OjaWs carve_oja(void* ws, size_t cap, int64_t b, int64_t d, int kp, size_t* tota
   if (s4 > sb) sb = s4;
   o.slab = c.take<float>(sb / sizeof(float) + 1);
   o.slab_bytes = sb;
+  o.ppart = c.take<float>((size_t)OB_NF * b * kp);
+  o.qpart = c.take<float>((size_t)OB_NR * d * kp);
+#ifdef DEIG_AB_OJA_TRACE
+  o.trace = c.take<unsigned long long>((size_t)OB_G * 64 * 16);
+#else
+  o.trace = nullptr;
+#endif
   *total = c.off;
   return o;
 }
@@ -522,20 +877,46 @@ size_t oja_workspace_bytes(int64_t b, int64_t d, int k) {
 // invertible k x k factor, so the span after every batch equals the one of
 // per-batch orthonormalisation (ref_cpu.oja_epoch); deferring it only lets the
 // column norms grow by ~(1 + eta lambda_max)^orth_every in between.
+// v4 (oja_blk_kernel) shape: one 4096-row batch on a 16 x 16 grid of X blocks held
+// in registers (d = 512 c <= 3072, kp <= 32), 256 co-resident workgroups.
+bool oja_blk_eligible(int64_t b, int64_t d, int64_t ldx, int kp) {
+  return b == (int64_t)OB_NR * OB_RB && d % 512 == 0 && d >= 512 && d <= 3072 && kp <= 32 &&
+         ldx % 4 == 0 && num_cus() >= OB_G;
+}
+
+template <int NB>
+void launch_oja_blk(int nks, const OjaBlk& a, hipStream_t st) {
+  switch (nks) {
+#define DEIG_OJA_NKS(x) \
+  case x:               \
+    hipLaunchKernelGGL((oja_blk_kernel<NB, x>), dim3(OB_G), dim3(512), 0, st, a); \
+    break;
+    DEIG_OJA_NKS(1) DEIG_OJA_NKS(2) DEIG_OJA_NKS(3) DEIG_OJA_NKS(4) DEIG_OJA_NKS(5) DEIG_OJA_NKS(6)
+#undef DEIG_OJA_NKS
+  }
+}
+
 int oja_steps_launch(const float* X, int64_t nb, int64_t b, int64_t d, int64_t ldx, float eta,
                      float* V, int k, int64_t ldv, int orth_every, void* ws, size_t ws_bytes,
-                     hipStream_t st) {
+                     hipStream_t st, int algo) {
   DEIG_REQUIRE(nb >= 1 && b >= 1 && d >= 4 && d % 4 == 0,
                "oja: need nb >= 1, b >= 1 and d %% 4 == 0");
   DEIG_REQUIRE(k >= 1 && k <= 64 && k <= d, "oja: need 1 <= k <= min(64, d)");
   DEIG_REQUIRE(ldx >= d && ldx % 4 == 0 && ldv >= d, "oja: bad leading dims");
   DEIG_REQUIRE(orth_every >= 1, "oja: orth_every must be >= 1");
+  DEIG_REQUIRE(algo == DEIG_OJA_AUTO || algo == DEIG_OJA_TWO_PASS || algo == DEIG_OJA_RESIDENT,
+               "oja: unknown algo %d", algo);
   const int kp = (int)cdiv(k, 16) * 16;
   size_t total = 0;
   OjaWs o = carve_oja(ws, ws_bytes, b, d, kp, &total);
   if (!ws || total > ws_bytes)
     return fail(DEIG_EWORKSPACE, "oja: workspace %zu < %zu", ws_bytes, total);
+  const bool blk = algo != DEIG_OJA_TWO_PASS && oja_blk_eligible(b, d, ldx, kp);
+  if (algo == DEIG_OJA_RESIDENT && !blk)
+    return fail(DEIG_EINVAL, "oja: the resident path needs b = 4096, d = 512 c <= 3072, k <= 32 "
+                             "and %d CUs (got b %lld, d %lld, k %d)", OB_G, (long long)b, (long long)d, k);
   int rc;
+  DEIG_HIP_CHECK(hipMemsetAsync(o.err, 0, sizeof(unsigned), st));
   // the basis lives in `cur` (o.Vr or o.Vr2: each CholQR pass swaps the two)
   float* cur = o.Vr;
   float* spare = o.Vr2;
@@ -551,11 +932,41 @@ int oja_steps_launch(const float* X, int64_t nb, int64_t b, int64_t d, int64_t l
     return DEIG_OK;
   };
   if ((rc = build_vimg(cur))) return rc;
-  for (int64_t i = 0; i < nb; ++i) {
-    const float* Xb = X + i * b * ldx;
-    // T = Xb V (as the TN pass's operand image, every row of its nkr k-steps written,
-    // zeros past b), then V += eta/b Xb^T T (and V's image)
-    switch (NB) {
+  // runs of batches between two re-orthonormalisations (after batch i when
+  // (i + 1) % orth_every == 0, and after the last): intermediate ones only bound the
+  // basis' condition number (the span is what the update carries) - one CholQR pass;
+  // the last one is CholQR2
+  for (int64_t i0 = 0; i0 < nb;) {
+    const int64_t i1 = std::min(nb, (i0 / orth_every + 1) * orth_every);
+    if (blk) {
+      DEIG_HIP_CHECK(hipMemsetAsync(o.cnt, 0, OB_CNT_BYTES, st));
+      OjaBlk a;
+      a.X = X + i0 * b * ldx;
+      a.ldx = ldx;
+      a.b = b;
+      a.d = (int)d;
+      a.kp = kp;
+      a.nbatch = (int)(i1 - i0);
+      a.coef = eta / (float)b;
+      a.V = cur;
+      a.vimg = o.vimg;
+      a.timg = o.timg;
+      a.ppart = o.ppart;
+      a.qpart = o.qpart;
+      a.cnt = o.cnt;
+      a.err = o.err;
+      a.trace = o.trace;
+      if (NB == 1)
+        launch_oja_blk<1>((int)(d / 512), a, st);
+      else
+        launch_oja_blk<2>((int)(d / 512), a, st);
+      DEIG_HIP_CHECK(hipGetLastError());
+    } else {
+      for (int64_t i = i0; i < i1; ++i) {
+        const float* Xb = X + i * b * ldx;
+        // T = Xb V (as the TN pass's operand image, every row of its nkr k-steps
+        // written, zeros past b), then V += eta/b Xb^T T (and V's image)
+        switch (NB) {
 #define DEIG_OJA_NB(x)                                                                           \
   case x:                                                                                        \
     hipLaunchKernelGGL(oja_nn_kernel<x>, dim3((unsigned)(2 * nkr)), dim3(512), 0, st, Xb, ldx, b, \
@@ -563,32 +974,31 @@ int oja_steps_launch(const float* X, int64_t nb, int64_t b, int64_t d, int64_t l
     hipLaunchKernelGGL(oja_tn_kernel<x>, dim3((unsigned)cdiv(d, 16)), dim3(512), 0, st, Xb, ldx, b, \
                        (int)d, nkr, o.timg, eta / (float)b, cur, o.vimg);                        \
     break;
-      DEIG_OJA_NB(1) DEIG_OJA_NB(2) DEIG_OJA_NB(3) DEIG_OJA_NB(4)
+          DEIG_OJA_NB(1) DEIG_OJA_NB(2) DEIG_OJA_NB(3) DEIG_OJA_NB(4)
 #undef DEIG_OJA_NB
-      default:
-        return fail(DEIG_EINVAL, "oja: k = %d > 64", k);
+          default:
+            return fail(DEIG_EINVAL, "oja: k = %d > 64", k);
+        }
+        DEIG_HIP_CHECK(hipGetLastError());
+      }
     }
-    DEIG_HIP_CHECK(hipGetLastError());
-    // intermediate re-orthonormalisations only bound the basis' condition number
-    // (the span is what the update carries): one CholQR pass; the last one is CholQR2
-    const int passes = (i + 1 == nb) ? 2 : ((i + 1) % orth_every == 0 ? 1 : 0);
-    if (passes) {
-      float* res = cur;
-      if ((rc = cholqr(cur, spare, o, d, k, kp, st, passes, &res))) return rc;
-      spare = res == cur ? spare : cur;
-      cur = res;
-      if (i + 1 < nb && (rc = build_vimg(cur))) return rc;
-    }
+    const int passes = i1 == nb ? 2 : 1;
+    float* res = cur;
+    if ((rc = cholqr(cur, spare, o, d, k, kp, st, passes, &res))) return rc;
+    spare = res == cur ? spare : cur;
+    cur = res;
+    if (i1 < nb && (rc = build_vimg(cur))) return rc;
+    i0 = i1;
   }
   hipLaunchKernelGGL(rowpad_to_col, dim3((unsigned)cdiv(d * k, 256)), dim3(256), 0, st, cur, d, k,
-                     kp, V, ldv);
+                     kp, V, ldv, o.err);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }
 
 int oja_launch(const float* Xb, int64_t b, int64_t d, int64_t ldx, float eta, float* V, int k,
                int64_t ldv, void* ws, size_t ws_bytes, hipStream_t st) {
-  return oja_steps_launch(Xb, 1, b, d, ldx, eta, V, k, ldv, 1, ws, ws_bytes, st);
+  return oja_steps_launch(Xb, 1, b, d, ldx, eta, V, k, ldv, 1, ws, ws_bytes, st, DEIG_OJA_AUTO);
 }
 
 }  // namespace deig

@@ -527,13 +527,15 @@ def oja_step(Xb: torch.Tensor, V: torch.Tensor, eta: float) -> torch.Tensor:
 
 
 def oja_steps(X: torch.Tensor, V: torch.Tensor, eta: float, batch: int,
-              orth_every: int = 8) -> torch.Tensor:
+              orth_every: int = 8, algo: str = "auto") -> torch.Tensor:
     """In-place Oja over the consecutive row batches X[i*batch:(i+1)*batch] (config 4).
 
     One C call for all batches (no host work in between); the basis is
     re-orthonormalised every ``orth_every`` batches and at the end, which gives the
     span of per-batch orthonormalisation (``oja_step`` in a loop) because the update
-    is linear in V.  Rows beyond the last full batch are ignored.  Returns V."""
+    is linear in V.  Rows beyond the last full batch are ignored.  ``algo``
+    (include/deig.h DEIG_OJA_*): "auto", "two_pass" or "resident" (Xb read once per
+    batch; batch = 4096, d a multiple of 512 up to 3072, k <= 32).  Returns V."""
     X = _rowmajor_4(require_device_tensor(X, "oja_steps"), "X")
     n, d = X.shape
     b = int(batch)
@@ -548,10 +550,10 @@ def oja_steps(X: torch.Tensor, V: torch.Tensor, eta: float, batch: int,
     with torch.cuda.device(X.device):
         nbytes = L.deig_oja_workspace(b, d, k)
         ws = _workspace(X.device, nbytes)
-        rc = L.deig_oja_steps_f32(X.data_ptr(), nb, b, d, X.stride(0), ctypes.c_float(eta),
-                                  V.data_ptr(), k, V.stride(1), int(orth_every), ws.data_ptr(),
-                                  nbytes, _stream(X.device))
-    _lib.check(rc, "deig_oja_steps_f32")
+        rc = L.deig_oja_steps_ex(X.data_ptr(), nb, b, d, X.stride(0), ctypes.c_float(eta),
+                                 V.data_ptr(), k, V.stride(1), int(orth_every),
+                                 _lib.OJA_ALGOS[algo], ws.data_ptr(), nbytes, _stream(X.device))
+    _lib.check(rc, "deig_oja_steps_ex")
     return V
 
 

@@ -305,6 +305,20 @@ int deig_oja_steps_f32(const float* X, int64_t nb, int64_t b, int64_t d, int64_t
                        float* V, int k, int64_t ldv, int orth_every, void* ws, size_t ws_bytes,
                        void* stream);
 
+/* deig_oja_steps_f32 with the algorithm chosen explicitly.  DEIG_OJA_AUTO (what
+ * deig_oja_steps_f32 does): the resident path where its shape allows, else the
+ * two-pass path.  DEIG_OJA_TWO_PASS: two launches per batch (Xb V, then Xb^T T: Xb
+ * read twice).  DEIG_OJA_RESIDENT: one launch per run of batches between two
+ * re-orthonormalisations, each workgroup holding its block of Xb in registers (Xb
+ * read once per batch); needs b = 4096, d a multiple of 512 up to 3072, k <= 32 and
+ * 256 CUs (DEIG_EINVAL otherwise).  Same workspace as deig_oja_steps_f32. */
+#define DEIG_OJA_AUTO 0
+#define DEIG_OJA_TWO_PASS 1
+#define DEIG_OJA_RESIDENT 2
+int deig_oja_steps_ex(const float* X, int64_t nb, int64_t b, int64_t d, int64_t ldx, float eta,
+                      float* V, int k, int64_t ldv, int orth_every, int algo, void* ws,
+                      size_t ws_bytes, void* stream);
+
 /* Projection onto an estimated eigenspace: Y = X W.
  * Replaces the notebook's  online_distributed_PCA = lambda X: X @ matrix_w
  * (Online Distributed PCA.ipynb raw line 345).  X: n x d row-major (ldx), W: d x k
