@@ -1,11 +1,13 @@
 // Mini-batch Oja steps for the online / streaming variant (BASELINE.json config 4):
 //   V <- orth(V + eta/b * Xb^T (Xb V)),   orth = Cholesky-QR2.
 // Not present in the reference (parity unpinned; judged by sin(theta) against
-// the one-shot float64 oracle and ref_cpu.oja_epoch).  Xb is read twice (Xb V
-// and Xb^T T), each pass at ~k/2 flop/B (HBM-bound for k <= 32): two launches per
-// batch (oja_nn_kernel, oja_tn_kernel), bf16x3 split products, K split over the
-// waves of a block and summed in LDS (no slab passes); each pass writes the next
-// one's MFMA operand image (T's for TN, V's for the next batch's NN).
+// the one-shot float64 oracle and ref_cpu.oja_epoch).  Two paths, bf16x3 split
+// products in both: the two-pass v3 (any shape) reads Xb twice (Xb V and Xb^T T),
+// two launches per batch (oja_nn_kernel, oja_tn_kernel), K split over the waves of a
+// block and summed in LDS (no slab passes), each pass writing the next one's MFMA
+// operand image (T's for TN, V's for the next batch's NN); the resident v4
+// (oja_blk_kernel, config 4's shape) runs a whole run of batches in one launch with
+// each workgroup's block of Xb held in registers - Xb read once per batch.
 #include <algorithm>
 
 #include "deig_internal.hpp"
