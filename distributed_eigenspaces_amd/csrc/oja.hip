@@ -75,8 +75,10 @@ __global__ __launch_bounds__(64) void chol_rinv_kernel(const float* __restrict__
   for (int j = 0; j < KP; ++j) {
     // pivot A[j][j] from lane j; L[r][j] = A[r][j] / L[j][j] for r > j
     const float v = fmaxf(__shfl(a[j], j, 64), 1e-12f * ref0);
-    const float ljj = sqrtf(v);
-    dinv[j] = 1.0f / ljj;
+    // one v_rsq_f32 (1 ulp) instead of the correctly rounded sqrt and division
+    // sequences: this single wave's latency chain is its cost
+    dinv[j] = __builtin_amdgcn_rsqf(v);
+    const float ljj = v * dinv[j];
     const float l = (r == j) ? ljj : (r > j ? a[j] * dinv[j] : 0.f);
     a[j] = l;
     if (live) col[r] = l;
