@@ -1385,14 +1385,23 @@ __global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ X,
 }
 
 // S[i][i] += alpha * sum_y corr[y][i]  (the dropped lo * lo term on the diagonal).
+// grid (d / 64): 64 features x 4 row slices per block, the slices summed in order
+// (r04: one thread per feature over all yb rows took 110 us at config 3 - 32 blocks,
+// each thread a 256-long dependent chain of loads; profiles/r04fin_c3_kernel_stats.csv)
 __global__ __launch_bounds__(256) void diag_corr_kernel(const float* __restrict__ corr, int yb,
                                                         int64_t dp, int d, float alpha, float* S,
                                                         int64_t lds) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= d) return;
+  __shared__ float part[4][64];
+  const int t = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + t;
   float c = 0.f;
-  for (int y = 0; y < yb; ++y) c += corr[(int64_t)y * dp + i];
-  S[(int64_t)i * lds + i] += alpha * c;
+  if (i < d) {
+#pragma unroll 8
+    for (int y = sl; y < yb; y += 4) c += corr[(int64_t)y * dp + i];
+  }
+  part[sl][t] = c;
+  __syncthreads();
+  if (sl == 0 && i < d) S[(int64_t)i * lds + i] += alpha * (((part[0][t] + part[1][t]) + part[2][t]) + part[3][t]);
 }
 
 // Lower-triangle tiles in super-tile order (SUPER_H tile rows x SUPER_W tile cols).
@@ -1651,7 +1660,7 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
       hipLaunchKernelGGL(syrks_reduce_kernel<16>, dim3(s.R, SLAB / 4 / 256), dim3(256), 0, stream, s);
       DEIG_HIP_CHECK(hipGetLastError());
     }
-    hipLaunchKernelGGL(diag_corr_kernel, dim3((unsigned)cdiv(d, 256)), dim3(256), 0, stream, corr,
+    hipLaunchKernelGGL(diag_corr_kernel, dim3((unsigned)cdiv(d, 64)), dim3(256), 0, stream, corr,
                        (int)yb, L.dp, (int)d, alpha, S, lds);
     DEIG_HIP_CHECK(hipGetLastError());
     return DEIG_OK;
@@ -1682,7 +1691,7 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
         hipLaunchKernelGGL(syrks_reduce_kernel<32>, dim3(s.R, SLAB / 4 / 256), dim3(256), 0, stream, s);
       DEIG_HIP_CHECK(hipGetLastError());
     }
-    hipLaunchKernelGGL(diag_corr_kernel, dim3((unsigned)cdiv(d, 256)), dim3(256), 0, stream, corr,
+    hipLaunchKernelGGL(diag_corr_kernel, dim3((unsigned)cdiv(d, 64)), dim3(256), 0, stream, corr,
                        (int)yb, L.dp, (int)d, alpha, S, lds);
     DEIG_HIP_CHECK(hipGetLastError());
   }
