@@ -1469,6 +1469,113 @@ __global__ __launch_bounds__(256) void rq_part_kernel(const T* __restrict__ S, i
   }  // groups
 }
 
+// r04: the quotients' products on f64 MFMA (v_mfma_f64_16x16x4_f64; fp32 S with
+// d % 4 == 0, lds % 4 == 0 and 16-B alignment - other inputs keep rq_part_kernel).
+// Persistent: 256 workgroups walk the lower 128 x 128 tiles of S (tile t -> row block
+// rb, column block cb <= rb).  Per tile W = S_tile V_cb (128 x kpad, on MFMA: wave w
+// owns rows 16 w .., all kpad / 16 vector tiles) and t_j += wgt sum_r V_rb[r][j] W[r][j]
+// (wgt 2 below the diagonal, 1 on it).  A operands straight from HBM: lane l loads
+// S[16 w + (l & 15)][16 q + 4 (l >> 4) .. + 3] and MFMA step (q, e) sums over the
+// columns 16 q + 4 g + e (g = l >> 4) - the k order is free as long as B follows it:
+// V_cb is staged in LDS as [vector][column] fp32 (row stride 132: conflict-free
+// 16-B reads) and lane l reads [16 nt + (l & 15)][16 q + 4 g ..].  Products of fp32
+// values are exact in double; sums in double, in a fixed order (deterministic).
+constexpr int RQM_T = 128, RQM_LDS = 132, RQM_G = 256;
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+template <int NT>
+__global__ __launch_bounds__(512) void rq_mfma_kernel(const float* __restrict__ S, int64_t lds, int64_t d,
+                                                      const float* __restrict__ V, int64_t ldv, int k,
+                                                      double* __restrict__ part) {
+  constexpr int KP = 16 * NT;  // kpad
+  __shared__ __attribute__((aligned(16))) float vc[KP][RQM_LDS];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c16 = lane & 15;
+  const int64_t nbk = cdiv(d, RQM_T);
+  const int64_t ntiles = nbk * (nbk + 1) / 2;
+  double tsum[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) tsum[nt] = 0.0;
+  for (int64_t ti = blockIdx.x; ti < ntiles; ti += gridDim.x) {
+    int64_t rb = (int64_t)((sqrt(8.0 * (double)ti + 1.0) - 1.0) * 0.5);
+    while (rb * (rb + 1) / 2 > ti) --rb;
+    while ((rb + 1) * (rb + 2) / 2 <= ti) ++rb;
+    const int64_t cb = ti - rb * (rb + 1) / 2;
+    const int64_t r0 = rb * RQM_T, c0 = cb * RQM_T;
+    const double wgt = rb > cb ? 2.0 : 1.0;
+    // this wave's A strip: 16 rows x 128 columns, one 16-column group ahead (clamped
+    // in range: rows past d meet zero V_rb values below, columns past d zero V_cb rows)
+    const int64_t row = r0 + 16 * w + c16;
+    const float* srow = S + (row < d ? row : d - 1) * lds;
+    auto load_a = [&](int q) {
+      const int64_t c = c0 + 16 * q + 4 * g;
+      return *reinterpret_cast<const f32x4*>(srow + (c < d ? c : d - 4));
+    };
+    f32x4 xn = load_a(0);
+    __syncthreads();  // the previous tile's vc reads are done
+    // V_cb -> LDS as [vector j][column]: zero for j >= k or columns past d
+    for (int u = tid; u < KP * (RQM_T / 4); u += 512) {
+      const int j = u / (RQM_T / 4), c4 = 4 * (u % (RQM_T / 4));
+      const int64_t c = c0 + c4;
+      f32x4 v = *reinterpret_cast<const f32x4*>(V + (int64_t)(j < k ? j : k - 1) * ldv + (c < d ? c : d - 4));
+      const float m = (j < k && c < d) ? 1.f : 0.f;
+      *reinterpret_cast<f32x4*>(&vc[j][c4]) = v * m;
+    }
+    __syncthreads();
+    f64x4 acc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[nt] = f64x4{0.0, 0.0, 0.0, 0.0};
+    constexpr int NG = NT < 4 ? NT : 4;  // vector tiles per B batch (independent accumulators)
+#pragma unroll 1
+    for (int q = 0; q < 8; ++q) {
+      const f32x4 xq = xn;
+      if (q < 7) xn = load_a(q + 1);  // one column group ahead
+      double a[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] = (double)xq[e];
+#pragma unroll
+      for (int n0 = 0; n0 < NT; n0 += NG) {
+        f32x4 bv[NG];
+#pragma unroll
+        for (int u = 0; u < NG && n0 + u < NT; ++u)
+          bv[u] = *reinterpret_cast<const f32x4*>(&vc[16 * (n0 + u) + c16][16 * q + 4 * g]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int u = 0; u < NG && n0 + u < NT; ++u)
+            acc[n0 + u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], (double)bv[u][e], acc[n0 + u], 0, 0, 0);
+      }
+    }
+    // epilogue: lane l holds W[16 w + g + 4 i][16 nt + c16] (f64 C/D map), i < 4
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int j = 16 * nt + c16;
+      const float* vj = V + (int64_t)(j < k ? j : k - 1) * ldv;
+      double t = 0.0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t r = r0 + 16 * w + g + 4 * i;
+        const double vr = (double)vj[r < d ? r : d - 1] * ((r < d && j < k) ? 1.0 : 0.0);
+        t = fma(vr, acc[nt][i], t);
+      }
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      tsum[nt] = fma(wgt, t, tsum[nt]);
+    }
+  }
+  // the 8 waves' sums in wave order -> part[block][j]
+  __shared__ double red[8][KP];
+  if (g == 0)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) red[w][16 * nt + c16] = tsum[nt];
+  __syncthreads();
+  if (tid < KP) {
+    double s = 0.0;
+#pragma unroll
+    for (int ww = 0; ww < 8; ++ww) s += red[ww][tid];
+    part[(int64_t)blockIdx.x * KP + tid] = s;
+  }
+}
+
 // block j: q = sum over the nblk parts (thread-strided, then a fixed LDS tree),
 // n = v^T v the same way; evals[j] = q / n.
 __global__ __launch_bounds__(256) void rq_finish_kernel(const double* __restrict__ part, int64_t nblk,
@@ -1633,18 +1740,32 @@ int rq_launch(const void* S, int stype, int64_t d, int64_t lds, const float* V, 
   double* part = Vd + d * kpad;
   const dim3 grid((unsigned)cdiv(d, RQ_CB), (unsigned)cdiv(d, RQ_RB));
   const int64_t nblk = (int64_t)grid.x * grid.y;
-  hipLaunchKernelGGL(rq_vd_kernel, dim3((unsigned)cdiv(d * kpad, 256)), dim3(256), 0, stream, V, ldv,
-                     d, k, kpad, Vd);
+  const bool mfma = stype == DEIG_F32 && d % 4 == 0 && lds % 4 == 0 && ldv % 4 == 0 && aligned16(S) &&
+                    aligned16(V) && d >= RQM_T && kpad <= 128;
+  if (mfma) {
+    const float* Sf = static_cast<const float*>(S);
+    switch (ng) {
+#define DEIG_RQM(x)                                                                                 \
+  case x:                                                                                           \
+    hipLaunchKernelGGL(rq_mfma_kernel<x>, dim3(RQM_G), dim3(512), 0, stream, Sf, lds, d, V, ldv, k, part); \
+    break;
+      DEIG_RQM(1) DEIG_RQM(2) DEIG_RQM(3) DEIG_RQM(4) DEIG_RQM(5) DEIG_RQM(6) DEIG_RQM(7) DEIG_RQM(8)
+#undef DEIG_RQM
+    }
+  } else {
+    hipLaunchKernelGGL(rq_vd_kernel, dim3((unsigned)cdiv(d * kpad, 256)), dim3(256), 0, stream, V, ldv,
+                       d, k, kpad, Vd);
+    DEIG_HIP_CHECK(hipGetLastError());
+    if (stype == DEIG_F64)
+      hipLaunchKernelGGL(rq_part_kernel<double>, grid, dim3(256), 0, stream,
+                         static_cast<const double*>(S), lds, d, Vd, V, ldv, k, ng, part);
+    else
+      hipLaunchKernelGGL(rq_part_kernel<float>, grid, dim3(256), 0, stream,
+                         static_cast<const float*>(S), lds, d, Vd, V, ldv, k, ng, part);
+  }
   DEIG_HIP_CHECK(hipGetLastError());
-  if (stype == DEIG_F64)
-    hipLaunchKernelGGL(rq_part_kernel<double>, grid, dim3(256), 0, stream,
-                       static_cast<const double*>(S), lds, d, Vd, V, ldv, k, ng, part);
-  else
-    hipLaunchKernelGGL(rq_part_kernel<float>, grid, dim3(256), 0, stream,
-                       static_cast<const float*>(S), lds, d, Vd, V, ldv, k, ng, part);
-  DEIG_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(rq_finish_kernel, dim3((unsigned)k), dim3(256), 0, stream, part, nblk, kpad, V,
-                     ldv, d, evals);
+  hipLaunchKernelGGL(rq_finish_kernel, dim3((unsigned)k), dim3(256), 0, stream, part,
+                     mfma ? (int64_t)RQM_G : nblk, kpad, V, ldv, d, evals);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
 }
