@@ -1158,6 +1158,96 @@ __global__ __launch_bounds__(256) void rr_update_kernel(float* __restrict__ Z, i
   }
 }
 
+// r04: the same update on fp32 MFMA (v_mfma_f32_16x16x4_f32: fp32 products and
+// sums, as the VALU form).  64 rows per block, wave w owns rows 16 w .. 16 w + 15 and
+// every 16-column tile of both products (Zq = Q W, Zy = Y W: 2 p / 16 accumulator
+// tiles).  Z's rows and W are staged in LDS (Z rows padded to 2 p + 1: the A reads,
+// lane l -> row l & 15, k = l >> 4, hit 16 distinct banks); the epilogue is the VALU
+// form's per element, the residual partials summed over lanes, then waves, in order.
+// (The VALU form reloads W - 64 KB at p = 128 - per 32 rows and reads LDS twice per
+// FMA pair: 575 us per 8-problem launch at d = 16384, p = 128, c5's timeline.)
+constexpr int URM = 64;
+
+template <int NC>  // NC = p / 16
+__global__ __launch_bounds__(256) void rr_update_mfma_kernel(float* __restrict__ Z, int64_t d, int k,
+                                                             const float* __restrict__ W,
+                                                             const float* __restrict__ lam,
+                                                             const float* __restrict__ cs,
+                                                             const float* __restrict__ qs, int64_t ldv,
+                                                             float* __restrict__ resid_part,
+                                                             const ProbBatch pbt) {
+  constexpr int P = 16 * NC, LD = 2 * P, LZ = 2 * P + 1;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* Ws = sm;               // P x P
+  float* Zs = sm + P * P;       // URM x LZ
+  float* rp = Zs + URM * LZ;    // 4 waves x P
+  const int prob = blockIdx.y;
+  float* __restrict__ V = pbt.V[prob];
+  if (prob) {
+    const int64_t o = pbt.off[prob];
+    Z = reinterpret_cast<float*>(reinterpret_cast<char*>(Z) + o);
+    W = reinterpret_cast<const float*>(reinterpret_cast<const char*>(W) + o);
+    lam = reinterpret_cast<const float*>(reinterpret_cast<const char*>(lam) + o);
+    cs = reinterpret_cast<const float*>(reinterpret_cast<const char*>(cs) + o);
+    qs = reinterpret_cast<const float*>(reinterpret_cast<const char*>(qs) + o);
+    resid_part = reinterpret_cast<float*>(reinterpret_cast<char*>(resid_part) + o);
+  }
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * URM;
+  for (int idx = tid; idx < P * P / 4; idx += 256)
+    *reinterpret_cast<f32x4*>(Ws + 4 * idx) = *reinterpret_cast<const f32x4*>(W + 4 * idx);
+  for (int idx = tid; idx < URM * LD / 4; idx += 256) {  // 16-B loads, padded rows
+    const int rr = idx / (LD / 4), c = 4 * (idx - rr * (LD / 4));
+    const int64_t row = r0 + rr;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(Z + (row < d ? row : d - 1) * LD + c);
+    const float m = row < d ? 1.f : 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) Zs[rr * LZ + c + e] = v[e] * m;
+  }
+  __syncthreads();
+  f32x4 aq[NC], ay[NC];
+#pragma unroll
+  for (int ct = 0; ct < NC; ++ct) aq[ct] = ay[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* zrow = Zs + (16 * w + (lane & 15)) * LZ + (lane >> 4);
+#pragma unroll 4
+  for (int k0 = 0; k0 < P; k0 += 4) {
+    const float a_q = zrow[k0], a_y = zrow[P + k0];
+    const float* wrow = Ws + (k0 + (lane >> 4)) * P + (lane & 15);
+#pragma unroll
+    for (int ct = 0; ct < NC; ++ct) {
+      const float b = wrow[16 * ct];
+      aq[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_q, b, aq[ct], 0, 0, 0);
+      ay[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_y, b, ay[ct], 0, 0, 0);
+    }
+  }
+  // C map: row 4 (lane >> 4) + i, column lane & 15
+#pragma unroll
+  for (int ct = 0; ct < NC; ++ct) {
+    const int j = 16 * ct + (lane & 15);
+    const float lj = lam[j], cj = cs[j], qj = qs[j];
+    float racc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = r0 + 16 * w + 4 * (lane >> 4) + i;
+      if (row < d) {
+        const float qw = aq[ct][i] * qj, yw = ay[ct][i] * qj;
+        if (j < k) {
+          const float e = yw - lj * qw;
+          racc = fmaf(e, e, racc);
+          V[row + (int64_t)(k - 1 - j) * ldv] = qw;
+        }
+        Z[row * LD + j] = (cj > 0.f) ? yw * (cj / qj) : qw;
+      }
+    }
+    racc += __shfl_xor(racc, 16, 64);
+    racc += __shfl_xor(racc, 32, 64);
+    if (lane < 16) rp[w * P + j] = racc;
+  }
+  __syncthreads();
+  for (int jj = tid; jj < k; jj += 256)
+    resid_part[(int64_t)blockIdx.x * k + jj] = ((rp[jj] + rp[P + jj]) + rp[2 * P + jj]) + rp[3 * P + jj];
+}
+
 // One wave per top-k column: lanes stride over the update blocks, shuffle-reduce
 // (fixed order, deterministic).
 __global__ __launch_bounds__(256) void rr_finish_kernel(const float* __restrict__ resid_part,
@@ -1792,15 +1882,35 @@ int rr_update_batch_launch(const RRBuffers& b, int64_t d, int p, int k, int64_t 
   const int nblk = rr_update_blocks(d);
   DEIG_REQUIRE(p >= 16 && p <= 128, "rr_update: p=%d out of range", p);
   DEIG_REQUIRE(pbt.n >= 1 && pbt.n <= kMaxProbBatch && pbt.off[0] == 0, "rr_update: batch of %d", pbt.n);
-  const size_t shm = (size_t)(p * p + UR * 2 * p + (256 / p) * k) * sizeof(float);
-  static const hipError_t attr = hipFuncSetAttribute(
-      (const void*)rr_update_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-      (int)((128 * 128 + UR * 256 + 16 * 128) * sizeof(float)));
-  DEIG_HIP_CHECK(attr);
-  hipLaunchKernelGGL(rr_update_kernel, dim3(nblk, pbt.n), dim3(256), shm, stream, b.Z, d, p, k, b.W,
-                     b.lam, b.cs, b.qs, ldv, b.resid_part, pbt);
+  // the MFMA form where its operands are 16-B aligned (p % 16 == 0 always holds)
+  const bool mfma = aligned16(b.W) && aligned16(b.Z) && (pbt.n == 1 || pbt.off[1] % 16 == 0);
+  const int nb = mfma ? (int)cdiv(d, URM) : nblk;
+  if (mfma) {
+    const size_t shm = (size_t)(p * p + URM * (2 * p + 1) + 4 * p) * sizeof(float);
+    switch (p / 16) {
+#define DEIG_RRU(x)                                                                                     \
+  case x: {                                                                                           \
+    static const hipError_t at = hipFuncSetAttribute((const void*)rr_update_mfma_kernel<x>,             \
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,        \
+                                                     (int)((16 * x * 16 * x + URM * (32 * x + 1) + 64 * x) * sizeof(float))); \
+    DEIG_HIP_CHECK(at);                                                                               \
+    hipLaunchKernelGGL(rr_update_mfma_kernel<x>, dim3(nb, pbt.n), dim3(256), shm, stream, b.Z, d, k, b.W, \
+                       b.lam, b.cs, b.qs, ldv, b.resid_part, pbt);                                    \
+  } break;
+      DEIG_RRU(1) DEIG_RRU(2) DEIG_RRU(3) DEIG_RRU(4) DEIG_RRU(5) DEIG_RRU(6) DEIG_RRU(7) DEIG_RRU(8)
+#undef DEIG_RRU
+    }
+  } else {
+    const size_t shm = (size_t)(p * p + UR * 2 * p + (256 / p) * k) * sizeof(float);
+    static const hipError_t attr = hipFuncSetAttribute(
+        (const void*)rr_update_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)((128 * 128 + UR * 256 + 16 * 128) * sizeof(float)));
+    DEIG_HIP_CHECK(attr);
+    hipLaunchKernelGGL(rr_update_kernel, dim3(nblk, pbt.n), dim3(256), shm, stream, b.Z, d, p, k, b.W,
+                       b.lam, b.cs, b.qs, ldv, b.resid_part, pbt);
+  }
   DEIG_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(rr_finish_kernel, dim3(pbt.n), dim3(256), 0, stream, b.resid_part, nblk, k,
+  hipLaunchKernelGGL(rr_finish_kernel, dim3(pbt.n), dim3(256), 0, stream, b.resid_part, nb, k,
                      b.lam, b.resid, pbt);
   DEIG_HIP_CHECK(hipGetLastError());
   return DEIG_OK;
