@@ -1405,15 +1405,24 @@ __global__ __launch_bounds__(256) void diag_corr_kernel(const float* __restrict_
 }
 
 // Lower-triangle tiles in super-tile order (SUPER_H tile rows x SUPER_W tile cols).
-__global__ void tile_order_kernel(int nt, int* order) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  int idx = 0;
-  for (int R0 = 0; R0 < nt; R0 += SUPER_H) {
-    const int rmax = R0 + SUPER_H < nt ? R0 + SUPER_H : nt;
-    for (int C0 = 0; C0 < rmax; C0 += SUPER_W)
-      for (int ti = R0; ti < rmax; ++ti)
-        for (int tj = C0; tj < C0 + SUPER_W && tj <= ti; ++tj) order[idx++] = ti | (tj << 16);
-  }
+// One thread per super-tile (r04: one thread for all took 110 us at d = 16384, 8 per
+// config-5 step): a super-row starts after the R0 (R0 + 1) / 2 tiles of the rows above,
+// a super-tile after its super-row's tiles left of it.
+__global__ __launch_bounds__(256) void tile_order_kernel(int nt, int* order) {
+  const int nsc = (nt + SUPER_W - 1) / SUPER_W;
+  const int u = blockIdx.x * 256 + threadIdx.x;
+  const int R0 = (u / nsc) * SUPER_H, C0 = (u % nsc) * SUPER_W;
+  if (R0 >= nt) return;
+  const int rmax = R0 + SUPER_H < nt ? R0 + SUPER_H : nt;
+  if (C0 >= rmax) return;
+  int idx = R0 * (R0 + 1) / 2;
+  for (int c = 0; c < C0; c += SUPER_W)
+    for (int ti = R0; ti < rmax; ++ti) {
+      const int hi = c + SUPER_W < ti + 1 ? c + SUPER_W : ti + 1;
+      idx += hi > c ? hi - c : 0;
+    }
+  for (int ti = R0; ti < rmax; ++ti)
+    for (int tj = C0; tj < C0 + SUPER_W && tj <= ti; ++tj) order[idx++] = ti | (tj << 16);
 }
 
 // K segments per remainder tile: the smallest nseg (<= 64) whose critical path
@@ -1633,7 +1642,8 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
 #endif
   s.xm = (int)L.xm;
   s.rpace = kSyrkRem & 1;
-  hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(64), 0, stream, s.nt,
+  hipLaunchKernelGGL(tile_order_kernel,
+                     dim3((unsigned)cdiv(cdiv(s.nt, SUPER_H) * cdiv(s.nt, SUPER_W), 256)), dim3(256), 0, stream, s.nt,
                      reinterpret_cast<int*>(base + L.off_order));
   DEIG_HIP_CHECK(hipGetLastError());
   s.X = X;
