@@ -48,7 +48,7 @@ __device__ __forceinline__ float lane_bcast(float v, int src) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
 }
 
-template <int KP>
+template <int KP, bool INV = true>
 __global__ __launch_bounds__(64) void chol_rinv_kernel(const float* __restrict__ G, int k, int kp,
                                                        float* __restrict__ Rinv) {
   // One wave; lane r keeps row r of the matrix in registers (static indices: the
@@ -94,6 +94,13 @@ __global__ __launch_bounds__(64) void chol_rinv_kernel(const float* __restrict__
     __syncthreads();
   }
   // lane r holds row r of L in a[0 .. r] (zeros above the diagonal)
+  if constexpr (!INV) {  // L itself (kp x kp, identity-padded beyond k) for trsm_img_kernel
+    if (r < kp)
+#pragma unroll
+      for (int c = 0; c < KP; ++c)
+        if (c < kp) Rinv[r * kp + c] = a[c];
+    return;
+  }
   if (live)
 #pragma unroll
     for (int c4 = 0; c4 < KP / 4; ++c4)
@@ -123,16 +130,6 @@ __global__ __launch_bounds__(64) void chol_rinv_kernel(const float* __restrict__
   }
 }
 
-void launch_chol_rinv(const float* G, int k, int kp, float* Rinv, hipStream_t st) {
-  if (kp <= 16)
-    hipLaunchKernelGGL(chol_rinv_kernel<16>, dim3(1), dim3(64), 0, st, G, k, kp, Rinv);
-  else if (kp <= 32)
-    hipLaunchKernelGGL(chol_rinv_kernel<32>, dim3(1), dim3(64), 0, st, G, k, kp, Rinv);
-  else if (kp <= 48)
-    hipLaunchKernelGGL(chol_rinv_kernel<48>, dim3(1), dim3(64), 0, st, G, k, kp, Rinv);
-  else
-    hipLaunchKernelGGL(chol_rinv_kernel<64>, dim3(1), dim3(64), 0, st, G, k, kp, Rinv);
-}
 
 // ---------------------------------------------------------------- v3 passes
 // bf16 operands for the split products of the NN pass (as the covariance and the
@@ -187,6 +184,70 @@ __global__ __launch_bounds__(256) void img_kernel(const float* __restrict__ M, i
   split8(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, hi, lo);
   img[img_index(ks, nb, 0, lane, NB)] = __builtin_bit_cast(u32x4, hi);
   img[img_index(ks, nb, 1, lane, NB)] = __builtin_bit_cast(u32x4, lo);
+}
+
+// V_out = V_in L^-T (the CholQR apply as a triangular solve: y L^T = v per row,
+// L from chol_rinv_kernel<KP, false>) and, with img != nullptr, V_out's NN operand
+// image (img_kernel's layout, fused).  One block per 32 rows (one image k-step); 8
+// lanes per row split each step's dot product (lane s takes the terms t = s mod 8) and
+// meet by xor shuffles, so every lane of the row knows y_i.  r04: replaces the
+// explicit inverse, the apply skinny pass and img_kernel.
+template <int KP>
+__global__ __launch_bounds__(256) void trsm_img_kernel(const float* __restrict__ Vin, const float* __restrict__ L,
+                                                       int64_t d, int kp, float* __restrict__ Vout,
+                                                       u32x4* __restrict__ img) {
+  __shared__ float Ls[KP][KP + 1];
+  __shared__ float dv[KP];
+  __shared__ float Ys[32][KP + 1];
+  const int t = threadIdx.x, rr = t >> 3, sub = t & 7;
+  const int64_t r0 = (int64_t)blockIdx.x * 32, row = r0 + rr;
+  for (int u = t; u < KP * KP; u += 256) {
+    const int i = u / KP, c = u - i * KP;
+    Ls[i][c] = (i < kp && c < kp) ? L[i * kp + c] : (i == c ? 1.f : 0.f);
+  }
+  for (int u = t; u < 32 * KP; u += 256) {
+    const int i = u / KP, c = u - i * KP;
+    const int64_t rw = r0 + i;
+    Ys[i][c] = (rw < d && c < kp) ? Vin[rw * kp + c] : 0.f;
+  }
+  __syncthreads();
+  if (t < KP) dv[t] = 1.0f / Ls[t][t];
+  __syncthreads();
+  float y[KP / 8];
+#pragma unroll
+  for (int tt = 0; tt < KP / 8; ++tt) y[tt] = 0.f;
+#pragma unroll
+  for (int i = 0; i < KP; ++i) {
+    float part = 0.f;
+#pragma unroll
+    for (int tt = 0; tt < (i + 7) / 8; ++tt)
+      if (8 * tt + sub < i) part = fmaf(Ls[i][8 * tt + sub], y[tt], part);
+    part += __shfl_xor(part, 1, 64);
+    part += __shfl_xor(part, 2, 64);
+    part += __shfl_xor(part, 4, 64);
+    const float yi = (Ys[rr][i] - part) * dv[i];
+    if ((i & 7) == sub) y[i / 8] = yi;
+  }
+  __syncthreads();  // every lane's reads of Ys are done
+#pragma unroll
+  for (int tt = 0; tt < KP / 8; ++tt) {
+    const int c = 8 * tt + sub;
+    Ys[rr][c] = y[tt];
+    if (row < d && c < kp) Vout[row * kp + c] = y[tt];
+  }
+  if (!img) return;
+  __syncthreads();
+  const int NB = kp / 16;
+  if (t < NB * 64) {  // image entries of k-step blockIdx.x: rows 8 (ln >> 4) .., column 16 nb + (ln & 15)
+    const int ln = t & 63, nb = t >> 6;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = Ys[8 * (ln >> 4) + j][16 * nb + (ln & 15)];
+    bf16x8 hi, lo;
+    split8(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, hi, lo);
+    img[img_index(blockIdx.x, nb, 0, ln, NB)] = __builtin_bit_cast(u32x4, hi);
+    img[img_index(blockIdx.x, nb, 1, ln, NB)] = __builtin_bit_cast(u32x4, lo);
+  }
 }
 
 // Measurement builds only (tools/oja_ab.py; the shipped library is variant 0):
@@ -843,8 +904,10 @@ OjaWs carve_oja(void* ws, size_t cap, int64_t b, int64_t d, int kp, size_t* tota
 // `passes` passes (2 = CholQR2, orthonormal to fp32 rounding; 1 = one pass, used
 // between batches where only the span and a bounded condition number matter);
 // the result is in *result (in or scratch: one buffer swap per pass).
+// The apply is a triangular solve (trsm_img_kernel) with L from the one-wave
+// Cholesky; with_img: the last pass also writes the result's NN operand image.
 int cholqr(float* in, float* scratch, const OjaWs& o, int64_t d, int k, int kp, hipStream_t st,
-           int passes, float** result) {
+           int passes, float** result, bool with_img) {
   int rc;
   float* cur = in;
   float* nxt = scratch;
@@ -852,11 +915,22 @@ int cholqr(float* in, float* scratch, const OjaWs& o, int64_t d, int k, int kp, 
     if ((rc = skinny_launch(true, cur, kp, cur, kp, o.G, kp, kp, kp, d, 1.f, 0.f, o.slab,
                             o.slab_bytes, st)))
       return rc;
-    launch_chol_rinv(o.G, k, kp, o.Rinv, st);
+    u32x4* img = (with_img && pass + 1 == passes) ? o.vimg : nullptr;
+    const dim3 g((unsigned)cdiv(d, 32));
+    if (kp <= 16) {
+      hipLaunchKernelGGL((chol_rinv_kernel<16, false>), dim3(1), dim3(64), 0, st, o.G, k, kp, o.Rinv);
+      hipLaunchKernelGGL(trsm_img_kernel<16>, g, dim3(256), 0, st, cur, o.Rinv, d, kp, nxt, img);
+    } else if (kp <= 32) {
+      hipLaunchKernelGGL((chol_rinv_kernel<32, false>), dim3(1), dim3(64), 0, st, o.G, k, kp, o.Rinv);
+      hipLaunchKernelGGL(trsm_img_kernel<32>, g, dim3(256), 0, st, cur, o.Rinv, d, kp, nxt, img);
+    } else if (kp <= 48) {
+      hipLaunchKernelGGL((chol_rinv_kernel<48, false>), dim3(1), dim3(64), 0, st, o.G, k, kp, o.Rinv);
+      hipLaunchKernelGGL(trsm_img_kernel<48>, g, dim3(256), 0, st, cur, o.Rinv, d, kp, nxt, img);
+    } else {
+      hipLaunchKernelGGL((chol_rinv_kernel<64, false>), dim3(1), dim3(64), 0, st, o.G, k, kp, o.Rinv);
+      hipLaunchKernelGGL(trsm_img_kernel<64>, g, dim3(256), 0, st, cur, o.Rinv, d, kp, nxt, img);
+    }
     DEIG_HIP_CHECK(hipGetLastError());
-    if ((rc = skinny_launch(false, cur, kp, o.Rinv, kp, nxt, kp, d, kp, kp, 1.f, 0.f, o.slab,
-                            o.slab_bytes, st)))
-      return rc;
     float* t = cur;
     cur = nxt;
     nxt = t;
@@ -988,10 +1062,9 @@ int oja_steps_launch(const float* X, int64_t nb, int64_t b, int64_t d, int64_t l
     }
     const int passes = i1 == nb ? 2 : 1;
     float* res = cur;
-    if ((rc = cholqr(cur, spare, o, d, k, kp, st, passes, &res))) return rc;
+    if ((rc = cholqr(cur, spare, o, d, k, kp, st, passes, &res, i1 < nb))) return rc;
     spare = res == cur ? spare : cur;
     cur = res;
-    if (i1 < nb && (rc = build_vimg(cur))) return rc;
     i0 = i1;
   }
   hipLaunchKernelGGL(rowpad_to_col, dim3((unsigned)cdiv(d * k, 256)), dim3(256), 0, st, cur, d, k,
