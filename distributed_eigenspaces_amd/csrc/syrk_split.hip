@@ -1373,8 +1373,11 @@ __global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ X,
       // [32-row block o/4][panel f/256][slice (o%4)*2 + hi|lo][f%256][16 B]
       unsigned char* dst = XP + ((o >> 2) * (dp / BT) + (f / BT)) * BLOCK_B +
                            ((o & 3) * 2) * SLICE_B + (f % BT) * 16;
-      *reinterpret_cast<u32x4*>(dst) = hv;
-      *reinterpret_cast<u32x4*>(dst + SLICE_B) = lv;
+      // non-temporal: the image is streamed back from HBM by the SYRK anyway (r04,
+      // profiles/r04zv_split_nt_stores_ab.log: config-3 shard 298.7 -> 297.8 ms per op,
+      // config 2 26.49 -> 26.33, bit-identical)
+      __builtin_nontemporal_store(hv, reinterpret_cast<u32x4*>(dst));
+      __builtin_nontemporal_store(lv, reinterpret_cast<u32x4*>(dst + SLICE_B));
     }
   }
 #pragma unroll
