@@ -185,40 +185,54 @@ def cpu_baseline_oneshot(xs: np.ndarray, n_worker: int, workers: int, k: int,
       the same rows (cpu_threaded_oneshot).
 
     ``value`` is the better of the two; both are reported."""
-    from oracle import ref_cpu
+    from threadpoolctl import threadpool_limits
     sample_rows, d = xs.shape
     cores = int(blas_cores())
-    t0 = time.perf_counter()
-    S = ref_cpu.sigma_hat(xs)
-    t_cov = time.perf_counter() - t0
-    de = min(d, EIGH_MAX_D)
-    t0 = time.perf_counter()
-    ref_cpu.top_k_eigh(S[:de, :de], k)
-    t_eig = (time.perf_counter() - t0) * (d / de) ** 3
-    del S
-    t_worker = t_cov * (n_worker / sample_rows) + t_eig
-    t_full = workers * t_worker
-    v1 = workers * n_worker / t_full
-    eig_note = (f"eigh top-{k} {t_eig:.2f}s" if de == d else
-                f"eigh top-{k} of the leading {de}x{de} block scaled by (d/{de})^3 -> {t_eig:.1f}s")
-    single = {"value": v1, "threads": 1, "blas_threads_per_worker": cores,
-              "note": (f"1 worker x {cores} BLAS threads on {sample_rows} rows x d={d} of a worker "
-                       f"shard: sigma_hat {t_cov:.2f}s + {eig_note}; covariance scaled linearly to "
-                       f"{n_worker} rows -> {t_worker:.1f}s per worker shard, x {workers} "
-                       f"worker(s)")}
+
+    def m1(nthreads):
+        """One worker on ``nthreads`` BLAS threads (None: the process default)."""
+        from oracle import ref_cpu
+        with threadpool_limits(limits=nthreads, user_api="blas"):
+            used = int(blas_cores())
+            t0 = time.perf_counter()
+            S = ref_cpu.sigma_hat(xs)
+            t_cov = time.perf_counter() - t0
+            de = min(d, EIGH_MAX_D)
+            t0 = time.perf_counter()
+            ref_cpu.top_k_eigh(S[:de, :de], k)
+            t_eig = (time.perf_counter() - t0) * (d / de) ** 3
+            del S
+        t_worker = t_cov * (n_worker / sample_rows) + t_eig
+        eig_note = (f"eigh top-{k} {t_eig:.2f}s" if de == d else
+                    f"eigh top-{k} of the leading {de}x{de} block scaled by (d/{de})^3 -> "
+                    f"{t_eig:.1f}s")
+        return {"value": workers * n_worker / (workers * t_worker), "threads": 1,
+                "blas_threads_per_worker": used,
+                "note": (f"1 worker x {used} BLAS threads on {sample_rows} rows x d={d} of a "
+                         f"worker shard: sigma_hat {t_cov:.2f}s + {eig_note}; covariance scaled "
+                         f"linearly to {n_worker} rows -> {t_worker:.1f}s per worker shard, x "
+                         f"{workers} worker(s)")}
+
+    single = m1(None)
+    # SURVEY.md §8(d)'s "m = 1 x all cores": every CPU of the host, whatever
+    # OMP_NUM_THREADS says (16 on the GPU box); BLAS may cap the count it really uses
+    nproc = os.cpu_count() or 1
+    allc = m1(nproc) if nproc > cores else None
     threaded = None
     if threads > 1:
         threaded = cpu_threaded_oneshot(xs, workers * n_worker, k, threads, cores,
                                         min(d, THREADED_EIGH_MAX_D))
-    best = threaded if threaded is not None and threaded["value"] > v1 else single
+    cands = [v for v in (single, allc, threaded) if v is not None]
+    best = max(cands, key=lambda v: v["value"])
     return {
-        "value": best["value"], "unit": "samples/s", "cores": cores, "kind": "port",
+        "value": best["value"], "unit": "samples/s", "cores": best["blas_threads_per_worker"]
+        * best["threads"], "kind": "port",
         "cpu_model": cpu_model(), "host": host_info(),
         "sample": (f"float64 NumPy/SciPy oracle (distributed.py:59-70 + :22-29) on a bounded "
-                   f"sample; best of: [{single['note']}]"
-                   + (f" and [{threaded['note']}]" if threaded else "")
+                   f"sample; best of: " + " and ".join(f"[{v['note']}]" for v in cands)
                    + "; server solve not counted"),
-        "variants": {"m1_all_cores": single, f"m{threads}_slave_threads": threaded},
+        "variants": {"m1_default_threads": single, "m1_all_cores": allc,
+                     f"m{threads}_slave_threads": threaded},
     }
 
 
@@ -259,27 +273,54 @@ def time_events(fn, reps: int, stream, trials: int = 1) -> float:
     return best
 
 
-def full_time_to_eigenspace(de, synthetic, X, U, n_total: int, k: int, stream) -> dict:
+SIGMA_SAMPLED_BAR = 2e-6   # sampled Sigma_hat vs float64 (north_star SYRK bar)
+EVAL_REL_BAR = 1e-5        # north_star: top-k eigenvalues to 1e-5 relative
+
+
+def spiked_block_fn(synthetic, U, first_seed: int = 1, seed0: int = 1000):
+    """Row block b of the streamed 16M-row job, generated in place: block 0 is the
+    bench shard itself (seed ``first_seed``), block b > 0 seed ``seed0 + b``."""
+    def gen(b, out):
+        synthetic.spiked_samples(out.shape[0], U, seed=first_seed if b == 0 else seed0 + b,
+                                 out=out)
+    return gen
+
+
+def full_time_to_eigenspace(de, gen_block, X, U, n_total: int, k: int, stream,
+                            keep_S: bool = False, f64_check: bool = True) -> dict:
     """BASELINE.json north_star's literal target on ONE GPU: the top-k eigenspace of
-    n_total = 16,777,216 rows of d = 8192.  They do not fit in HBM (512 GiB of
-    fp32), so they stream through the covariance in blocks of X's rows, each block
-    accumulated into one Sigma (DEIG_SYRK_ACCUMULATE; the block is regenerated in
-    place between blocks - a data-arrival stand-in, untimed), then one eigensolve.
-    Timed: the covariance launches (HIP events on the launch stream) + the solve."""
+    n_total = 16,777,216 rows of d = 8192 (reference/distributed.py:66-69 forms
+    Sigma_hat of any n in one call, then :22-29 its top-k).  The rows do not fit in HBM
+    (512 GiB of fp32), so they stream through the covariance in blocks of X's rows,
+    each block accumulated into one Sigma (block 0 overwrites S, the others
+    DEIG_SYRK_ACCUMULATE; ``gen_block(b, X)`` regenerates block b in place - a
+    data-arrival stand-in, untimed), then one eigensolve.
+
+    Timed: each block's ONE covariance launch (one HIP event pair on the launch
+    stream around the single call - r04 timed it with ``time_events``, whose warm-up
+    call accumulated every block twice, S = 2 Sigma_hat) + the solve.
+
+    Checked (outside the timed launches; raises if a bar is missed): a float64 X^T X
+    of 16 sampled features over all rows vs the same entries of S (<= 2e-6), and -
+    after the solve, with the blocks regenerated - the float64 Rayleigh quotients
+    v_j^T Sigma v_j and residuals ||Sigma v_j - rq_j v_j|| / lambda_max of the returned
+    vectors on the float64 Sigma of ALL rows (never formed: X V, then X^T (X V),
+    block by block), against the returned eigenvalues (<= 1e-5 relative)."""
     n, d = X.shape
     blocks = n_total // n
-    S = torch.zeros((d, d), dtype=torch.float32, device=X.device)
-    # accuracy of the streamed Sigma: a float64 X^T X of 16 sampled features over all
-    # 2^24 rows, accumulated block by block outside the timed launches
+    S = torch.empty((d, d), dtype=torch.float32, device=X.device)
     cols = torch.randperm(d, generator=torch.Generator().manual_seed(7))[:16].to(X.device)
     S64 = torch.zeros((16, 16), dtype=torch.float64, device=X.device)
     syrk_ms = []
     for b in range(blocks):
-        if b > 0:
-            synthetic.spiked_samples(n, U, seed=1000 + b, out=X)
+        gen_block(b, X)
         torch.cuda.synchronize()
-        syrk_ms.append(time_events(lambda: de.sigma_hat(X, alpha=1.0 / n_total, out=S,
-                                                        accumulate=True), 1, stream))
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        de.sigma_hat(X, alpha=1.0 / n_total, out=S, accumulate=b > 0)
+        e1.record(stream)
+        e1.synchronize()
+        syrk_ms.append(e0.elapsed_time(e1))
         Xc = X.index_select(1, cols).double()
         S64 += Xc.t() @ Xc
         del Xc
@@ -292,15 +333,49 @@ def full_time_to_eigenspace(de, synthetic, X, U, n_total: int, k: int, stream) -
     torch.cuda.synchronize()
     solve_s = time.perf_counter() - t0
     cov_s = float(sum(syrk_ms)) / 1e3
-    return {"rows": n_total, "d": d, "k": k, "blocks": blocks, "rows_per_block": n,
-            "covariance_s": cov_s, "solve_s": solve_s, "time_to_eigenspace_s": cov_s + solve_s,
-            "samples_per_s": n_total / (cov_s + solve_s), "sweeps": r.sweeps, "resid": r.resid,
-            "sin_theta_vs_planted": sin_theta(U, r.V),
-            "sigma_hat_rel_err_vs_f64_sampled": sigma_err,
-            "note": "one GPU streams all 2^24 rows (config 3's total) through one covariance "
-                    "(DEIG_SYRK_ACCUMULATE, tests/test_gpu_syrk_chunks.py); block regeneration "
-                    "between launches is untimed (data arrival); sigma_hat_rel_err_vs_f64_sampled: "
-                    "16 sampled features, float64 over all rows"}
+    out = {"rows": n_total, "d": d, "k": k, "blocks": blocks, "rows_per_block": n,
+           "covariance_s": cov_s, "covariance_ms_per_block": syrk_ms, "solve_s": solve_s,
+           "time_to_eigenspace_s": cov_s + solve_s,
+           "samples_per_s": n_total / (cov_s + solve_s), "sweeps": r.sweeps, "resid": r.resid,
+           "sin_theta_vs_planted": sin_theta(U, r.V),
+           "sigma_hat_rel_err_vs_f64_sampled": sigma_err,
+           "evals": [float(v) for v in r.evals.cpu()]}
+    if sigma_err > SIGMA_SAMPLED_BAR:
+        raise RuntimeError(f"16M-row Sigma_hat: sampled rel err {sigma_err:.3e} > "
+                           f"{SIGMA_SAMPLED_BAR:.0e} vs float64 - not the reference's Sigma_hat")
+    if f64_check:
+        V64 = r.V.double()
+        Z = torch.zeros((d, k), dtype=torch.float64, device=X.device)
+        ch = 1 << 17
+        for b in range(blocks):
+            gen_block(b, X)
+            for lo in range(0, n, ch):
+                Xd = X[lo:lo + ch].double()
+                Z.addmm_(Xd.t(), Xd @ V64)
+                del Xd
+        Z /= n_total
+        vn = (V64 * V64).sum(0)
+        rq = (V64 * Z).sum(0) / vn
+        res = (Z - V64 * rq[None, :]).norm(dim=0) / vn.sqrt()
+        lam_max = float(rq.abs().max())
+        ev_err = float(((r.evals.double() - rq).abs() / rq.abs()).max())
+        out.update({"evals_rel_err_vs_f64_rayleigh_all_rows": ev_err,
+                    "resid_vs_f64_sigma_all_rows": float(res.max() / lam_max)})
+        if ev_err > EVAL_REL_BAR:
+            raise RuntimeError(f"16M-row eigenvalues: rel err {ev_err:.3e} vs the float64 "
+                               f"Rayleigh quotients on all rows > {EVAL_REL_BAR:.0e}")
+    out["note"] = ("one GPU streams all n_total rows (config 3's 2^24) through one covariance "
+                   "(block 0 overwrites, the rest DEIG_SYRK_ACCUMULATE; "
+                   "tests/test_gpu_syrk_chunks.py::test_full_time_to_eigenspace_helper); each "
+                   "block's single launch timed by one HIP event pair; block regeneration "
+                   "between launches is untimed (data arrival); sigma_hat_rel_err_vs_f64_sampled: "
+                   "16 sampled features, float64 over all rows (bar 2e-6); "
+                   "evals_rel_err_vs_f64_rayleigh_all_rows / resid_vs_f64_sigma_all_rows: the "
+                   "returned pairs against the float64 Sigma_hat of ALL rows (bar 1e-5)")
+    if keep_S:
+        out["S"] = S
+        out["V"] = r.V
+    return out
 
 
 def sweep_roofline(de, S: torch.Tensor, p: int, stream) -> dict:
@@ -740,7 +815,8 @@ def run_oneshot(args, cfg, world, rank, dev):
                                    ni, W, k)
     full = None
     if cfg.get("full_rows") and world == 1 and not args.rows and not args.no_full:
-        full = full_time_to_eigenspace(de, synthetic, X[:ni], U, cfg["full_rows"], k, stream)
+        full = full_time_to_eigenspace(de, spiked_block_fn(synthetic, U), X[:ni], U,
+                                       cfg["full_rows"], k, stream)
     line = base_line(args, world, elapsed, float(n) * world * args.steps, "u8" if u8 else "f32", {
         "workload": cfg["label"], "rows_per_gpu": n, "total_rows": n * world, "d": d, "k": k,
         "workers_per_gpu": W, "rows_per_worker": ni, "workers_total": m, "subspace_p": p,
@@ -835,8 +911,11 @@ def run_oja(args, cfg, world, rank, dev):
     # the last Oja batch's end (r03's host clock started when the 64 batches were
     # enqueued, so it also counted their GPU time)
     agg_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
-    byt = 8.0 * b * d  # Xb read twice (Xb V, then Xb^T T)
+    # an Oja batch's algorithmic HBM bytes are ONE read of Xb (4·b·d);
+    # the two-pass path reads it twice (that is its cost, not the algorithm's)
+    byt = 4.0 * b * d
     achieved = byt / (oja_ms * 1e-3)
+    fl = 4.0 * b * d * k  # Xb·V and Xbᵀ·T: 2·b·d·k flop each
     if rank != 0:
         return None
     cpu = None
@@ -857,9 +936,15 @@ def run_oja(args, cfg, world, rank, dev):
     line["roofline"] = {"bound": "hbm", "kernel": kname,
                         "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK, "traffic": None,
-                        "algorithmic": f"8*b*d = {byt:.4e} bytes per batch (the two products each "
-                                       "stream Xb; the resident path reads it from HBM once)",
-                        "launch_ms": oja_ms}
+                        "algorithmic": f"4*b*d = {byt:.4e} bytes per batch (Xb read from HBM "
+                                       "once, SURVEY.md §8(d); V / T are L2-resident)",
+                        "launch_ms": oja_ms,
+                        "mfma_leg": {"flop_per_batch": fl,
+                                     "bf16_mfma_flop_per_batch": 3 * fl,
+                                     "achieved_bf16_tflops": 3 * fl / (oja_ms * 1e-3) / 1e12,
+                                     "frac_of_bf16_peak": 3 * fl / (oja_ms * 1e-3) / BF16_MFMA_PEAK,
+                                     "note": "4·b·d·k fp32-equivalent flop per batch, each formed "
+                                             "from 3 bf16 MFMA products (bf16x3)"}}
     line["cpu_baseline"] = cpu
     line["breakdown"] = {"oja_ms_per_batch": oja_ms,
                          "aggregate_ms": agg_ms,

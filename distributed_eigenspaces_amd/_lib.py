@@ -101,9 +101,16 @@ SIGNATURES = {
                                            _c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_float, ctypes.POINTER(_vp), _c_i64,
                                            ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_int),
-                                           ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int),
+                                           ctypes.POINTER(ctypes.c_float),
                                            ctypes.POINTER(SolverOpts), _vp, _c_sz,
                                            ctypes.POINTER(_vp), _vp]),
+    "deig_topk_sym_batch_ex": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp), ctypes.c_int, _c_i64,
+                                              _c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_float, ctypes.POINTER(_vp), _c_i64,
+                                              ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_int),
+                                              ctypes.POINTER(ctypes.c_float),
+                                              ctypes.POINTER(ctypes.c_int),
+                                              ctypes.POINTER(SolverOpts), _vp, _c_sz, _vp]),
     "deig_projavg_topk_ex": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, ctypes.c_float,
                                             ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_float, _fp, ctypes.c_int, _c_i64, _fp,

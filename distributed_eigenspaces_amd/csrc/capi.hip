@@ -408,6 +408,11 @@ struct Solver {
   bool allow_early = false, early = false;
   int rr_every = 4, jcap_sweeps = 2, jcap = 30, nrr = 0, start = 0, since_best = 0;
   float tau = 0.f, jcap_above = 1e-4f, best = 3.4e38f;
+  // |theta| scale of the whole operator (the first block's Ritz values; 0 until the
+  // first block has ended) and the factor that turns the last RR's residuals from
+  // "relative to the block's own largest Ritz value" (rr_finish_kernel) into
+  // "relative to the operator's scale" - 1 outside the deflation-residue band
+  float abs_scale = 0.f, band_f = 1.f;
   bool fuse = false;
   int ncheb_dbg = 0;
 
@@ -574,7 +579,17 @@ struct Solver {
   int cycle_finish(bool* done) {
     *done = false;
     jconv_h = jcap < 30 ? hs->jconv : 1;
-    last = res_h[kc];
+    // A block in the deflation-residue band - every Ritz value ~0 next to the
+    // operator's scale: a rank-deficient S with k above its rank, or k close to d,
+    // after the locked pairs were deflated to ~0 - has residuals relative to its own
+    // ~0 Ritz values, which never fall below tol.  It is judged by the documented
+    // criterion instead (include/deig.h): ||S v - lambda v|| / |lambda_max(S)|.
+    band_f = 1.f;
+    if (abs_scale > 0.f) {
+      const float blk = fmaxf(fabsf(lam_h[0]), 1e-30f);
+      if (blk <= kNegRel * abs_scale) band_f = blk / abs_scale;
+    }
+    last = res_h[kc] * band_f;
     // Ritz pairs of a capped Jacobi that stopped short are approximate: their
     // residual bounds the error, but the eigenvalues / vectors returned are those
     // of an unconverged small solve, so no exit is taken on them - the next RR
@@ -606,7 +621,7 @@ struct Solver {
     if (allow_early) {
       const int r = dominant(kc);
       bool ok = r >= 1;
-      for (int j = 0; j < r && ok; ++j) ok = res_h[j] <= tol;
+      for (int j = 0; j < r && ok; ++j) ok = res_h[j] * band_f <= tol;
       if (ok) {
         early = true;
         *done = true;
@@ -954,6 +969,7 @@ struct SolveSM {
       if (band && (r = block_mgs_launch(Vb, ldv, d, kc, sv.st))) return r;
     }
     if (locked == 0 && attempt == 0) scale = fmaxf(fabsf(sv.lam_h[0]), fabsf(sv.lam_h[pb - 1]));
+    sv.abs_scale = scale;
     // Indefinite S: the most negative Ritz value of the block against the block's
     // target (and the operator's scale - deflation residue is ~1e-7 of it).
     const float tmin = sv.lam_h[pb - 1];
@@ -1276,7 +1292,7 @@ using namespace deig;
 
 extern "C" {
 
-int deig_version(void) { return 0x000400; }
+int deig_version(void) { return 0x000500; }
 
 const char* deig_last_error(void) { return g_err; }
 
@@ -1439,9 +1455,17 @@ size_t deig_topk_batch_workspace(int W, int64_t d, int k, int p, int stype,
 
 int deig_topk_sym_batch(int W, const void* const* S, int stype, int64_t d, int64_t lds, int k, int p,
                         int max_sweeps, float tol, float* const* V, int64_t ldv, float* const* evals,
-                        int* sweeps_out, float* resid_out, int* status_out,
-                        const deig_solver_opts* opts, void* ws, size_t ws_bytes,
-                        void* const* streams, void* stream) {
+                        int* sweeps_out, float* resid_out, const deig_solver_opts* opts, void* ws,
+                        size_t ws_bytes, void* const* streams, void* stream) {
+  (void)streams;  // r03's per-problem streams: every launch is on `stream` since r04
+  return deig_topk_sym_batch_ex(W, S, stype, d, lds, k, p, max_sweeps, tol, V, ldv, evals, sweeps_out,
+                                resid_out, nullptr, opts, ws, ws_bytes, stream);
+}
+
+int deig_topk_sym_batch_ex(int W, const void* const* S, int stype, int64_t d, int64_t lds, int k, int p,
+                           int max_sweeps, float tol, float* const* V, int64_t ldv,
+                           float* const* evals, int* sweeps_out, float* resid_out, int* status_out,
+                           const deig_solver_opts* opts, void* ws, size_t ws_bytes, void* stream) {
   g_err[0] = 0;
   if (int rc = check_opts(opts)) return rc;
   if (W < 1 || !S || !V || !evals) return fail(DEIG_EINVAL, "topk_batch: need W >= 1 and S / V / evals arrays");
@@ -1453,7 +1477,6 @@ int deig_topk_sym_batch(int W, const void* const* S, int stype, int64_t d, int64
   if (!ws || ws_bytes < (size_t)W * each)
     return fail(DEIG_EWORKSPACE, "topk_batch: workspace %zu bytes < required %zu", ws_bytes,
                 (size_t)W * each);
-  (void)streams;  // r03's per-problem streams: every launch is on `stream` since r04
   std::vector<Operator> ops(W);
   for (int i = 0; i < W; ++i) {
     ops[i] = Operator{};

@@ -962,16 +962,25 @@ bool oja_blk_eligible(int64_t b, int64_t d, int64_t ldx, int kp) {
          ldx % 4 == 0 && num_cus() >= OB_G;
 }
 
+// The resident kernel's workgroups wait on each other, so all OB_G of them must be
+// resident at once: a cooperative launch, which the runtime refuses (instead of
+// starting a grid that could deadlock until the 2-s spin bound) when they cannot be.
 template <int NB>
-void launch_oja_blk(int nks, const OjaBlk& a, hipStream_t st) {
+hipError_t launch_oja_blk(int nks, const OjaBlk& a, hipStream_t st) {
+  const void* fn = nullptr;
   switch (nks) {
 #define DEIG_OJA_NKS(x) \
   case x:               \
-    hipLaunchKernelGGL((oja_blk_kernel<NB, x>), dim3(OB_G), dim3(512), 0, st, a); \
+    fn = reinterpret_cast<const void*>(&oja_blk_kernel<NB, x>); \
     break;
     DEIG_OJA_NKS(1) DEIG_OJA_NKS(2) DEIG_OJA_NKS(3) DEIG_OJA_NKS(4) DEIG_OJA_NKS(5) DEIG_OJA_NKS(6)
 #undef DEIG_OJA_NKS
+    default:
+      return hipErrorInvalidValue;
   }
+  OjaBlk arg = a;
+  void* args[] = {&arg};
+  return hipLaunchCooperativeKernel(fn, dim3(OB_G), dim3(512), args, 0, st);
 }
 
 int oja_steps_launch(const float* X, int64_t nb, int64_t b, int64_t d, int64_t ldx, float eta,
@@ -989,7 +998,7 @@ int oja_steps_launch(const float* X, int64_t nb, int64_t b, int64_t d, int64_t l
   OjaWs o = carve_oja(ws, ws_bytes, b, d, kp, &total);
   if (!ws || total > ws_bytes)
     return fail(DEIG_EWORKSPACE, "oja: workspace %zu < %zu", ws_bytes, total);
-  const bool blk = algo != DEIG_OJA_TWO_PASS && oja_blk_eligible(b, d, ldx, kp);
+  bool blk = algo != DEIG_OJA_TWO_PASS && oja_blk_eligible(b, d, ldx, kp);
   if (algo == DEIG_OJA_RESIDENT && !blk)
     return fail(DEIG_EINVAL, "oja: the resident path needs b = 4096, d = 512 c <= 3072, k <= 32 "
                              "and %d CUs (got b %lld, d %lld, k %d)", OB_G, (long long)b, (long long)d, k);
@@ -1034,12 +1043,20 @@ int oja_steps_launch(const float* X, int64_t nb, int64_t b, int64_t d, int64_t l
       a.cnt = o.cnt;
       a.err = o.err;
       a.trace = o.trace;
-      if (NB == 1)
-        launch_oja_blk<1>((int)(d / 512), a, st);
-      else
-        launch_oja_blk<2>((int)(d / 512), a, st);
-      DEIG_HIP_CHECK(hipGetLastError());
-    } else {
+      const hipError_t le = NB == 1 ? launch_oja_blk<1>((int)(d / 512), a, st)
+                                    : launch_oja_blk<2>((int)(d / 512), a, st);
+      if (le != hipSuccess) {
+        (void)hipGetLastError();
+        // the grid cannot be co-resident (CUs held by other work, a partitioned
+        // device): DEIG_OJA_RESIDENT reports it, AUTO runs this and every later run
+        // on the two-pass kernels (the same arithmetic, to within 1e-5)
+        if (algo == DEIG_OJA_RESIDENT)
+          return fail(DEIG_EHIP, "oja: cooperative launch of the resident kernel refused: %s",
+                      hipGetErrorString(le));
+        blk = false;
+      }
+    }
+    if (!blk) {
       for (int64_t i = i0; i < i1; ++i) {
         const float* Xb = X + i * b * ldx;
         // T = Xb V (as the TN pass's operand image, every row of its nkr k-steps

@@ -1818,8 +1818,12 @@ int block_mgs_launch(float* V, int64_t ldv, int64_t d, int kc, hipStream_t strea
 }
 
 size_t rq_workspace_bytes(int64_t d, int k) {
+  // part[] holds one kpad-row per block of whichever kernel rq_launch picks: the VALU
+  // form's grid (nblk) or the MFMA form's fixed RQM_G workgroups (more than nblk for
+  // d below ~1020)
   const int64_t nblk = cdiv(d, RQ_CB) * cdiv(d, RQ_RB);
-  return (size_t)(d + nblk) * cdiv(k, RQ_KG) * RQ_KG * sizeof(double);
+  const int64_t nprt = nblk > RQM_G ? nblk : (int64_t)RQM_G;
+  return (size_t)(d + nprt) * cdiv(k, RQ_KG) * RQ_KG * sizeof(double);
 }
 
 int rq_launch(const void* S, int stype, int64_t d, int64_t lds, const float* V, int64_t ldv, int k,

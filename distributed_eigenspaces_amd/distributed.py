@@ -94,12 +94,16 @@ def _device_copy(data) -> torch.Tensor:
     if not torch.cuda.is_available():
         raise RuntimeError("SlaveNode: needs a ROCm GPU; there is no CPU fallback")
     if isinstance(data, np.ndarray):
-        # a read-only array that owns its memory cannot change: no sampling pass
-        owned_ro = not data.flags.writeable and data.base is None
-        fp = (data.shape, data.dtype.str, "ro") if owned_ro else _fingerprint(data)
+        # always sampled: a read-only flag can be switched back on, written and locked
+        fp = _fingerprint(data)
     elif isinstance(data, torch.Tensor):
-        # a CPU tensor: its storage and in-place version counter say whether it changed
-        fp = (tuple(data.shape), str(data.dtype), data.data_ptr(), data._version)
+        # a CPU tensor: storage, in-place version counter AND the sampled contents
+        # (writes through an aliasing numpy array or raw pointers bypass _version)
+        try:
+            content = _fingerprint(data.detach().numpy())
+        except (TypeError, RuntimeError):  # a dtype numpy cannot view: never cached
+            content = None
+        fp = None if content is None else (data.data_ptr(), data._version, content)
     else:
         fp = None  # other array-likes: converted on every call, never cached
     key = id(data)

@@ -434,12 +434,13 @@ def topk_eigh_batch(Ss, k: int, *, p: int | None = None, tol: float = DEFAULT_TO
     with torch.cuda.device(dev):
         nbytes = L.deig_topk_batch_workspace(W, d, k, pp, stype, ctypes.byref(o))
         ws = _workspace(dev, nbytes)
-        rc = L.deig_topk_sym_batch(W, S_arr, stype, d, lds, k, pp, int(max_sweeps), ctypes.c_float(tol),
-                                   V_arr, d, E_arr, sweeps, resid, status, ctypes.byref(o),
-                                   ws.data_ptr(), nbytes, None, cur.cuda_stream)
-    _lib.check(rc, "deig_topk_sym_batch")
+        rc = L.deig_topk_sym_batch_ex(W, S_arr, stype, d, lds, k, pp, int(max_sweeps),
+                                      ctypes.c_float(tol), V_arr, d, E_arr, sweeps, resid, status,
+                                      ctypes.byref(o), ws.data_ptr(), nbytes, cur.cuda_stream)
+    _lib.check(rc, "deig_topk_sym_batch_ex")
     if rc != _lib.DEIG_OK:
-        warnings.warn(f"deig_topk_sym_batch: {_lib.last_error()}", _lib.NotConvergedWarning, stacklevel=2)
+        warnings.warn(f"deig_topk_sym_batch_ex: {_lib.last_error()}", _lib.NotConvergedWarning,
+                      stacklevel=2)
     # each problem's own outcome (status[i]: what deig_topk_sym_ex would have returned)
     return [EigResult(evals=evs[i], V=Vs[i], sweeps=int(sweeps[i]), resid=float(resid[i]),
                       converged=int(status[i]) == _lib.DEIG_OK) for i in range(W)]

@@ -262,21 +262,27 @@ int deig_projavg_topk_f32(const float* Wt, int64_t d, int64_t mk, int64_t ldw,
  * is enqueued as batched launches on `stream` (the sweeps of all problems at the same
  * point of their plans in one launch per kernel, one Gram, one small-solve launch of
  * one workgroup per problem, one update) and one stream sync serves every problem's
- * host decisions.  streams: ignored since 0x000400 (r03: per-problem streams; kept
- * for the ABI, may be NULL).  All work is ordered on
- * `stream`.  Workspace: deig_topk_batch_workspace(W, ...) bytes.  Returns the
- * first error; DEIG_NOT_CONVERGED if any problem stopped above tol.  status_out[i]
- * (host array, may be NULL): problem i's own return code, the one deig_topk_sym_ex
- * would have returned for it.
+ * host decisions.  All work is ordered on `stream`.  Workspace:
+ * deig_topk_batch_workspace(W, ...) bytes.  Returns the first error;
+ * DEIG_NOT_CONVERGED if any problem stopped above tol.  status_out[i] (host array,
+ * may be NULL): problem i's own return code, the one deig_topk_sym_ex would have
+ * returned for it.
  * Replaces W concurrent Node.top_k_eigenvectors calls (distributed.py:22-29, one
  * per SlaveNode shard :42-53). */
 size_t deig_topk_batch_workspace(int W, int64_t d, int k, int p, int stype,
                                  const deig_solver_opts* opts);
+int deig_topk_sym_batch_ex(int W, const void* const* S, int stype, int64_t d, int64_t lds, int k, int p,
+                           int max_sweeps, float tol, float* const* V, int64_t ldv,
+                           float* const* evals, int* sweeps_out, float* resid_out, int* status_out,
+                           const deig_solver_opts* opts, void* ws, size_t ws_bytes, void* stream);
+/* The r03 (0x000300) signature, unchanged: deig_topk_sym_batch_ex with
+ * status_out = NULL.  streams: ignored since 0x000400 (r03 ran one stream per
+ * problem; may be NULL).  (0x000400 had inserted status_out into THIS signature, an
+ * in-place ABI break; 0x000500 restores it and moves status_out to the _ex form.) */
 int deig_topk_sym_batch(int W, const void* const* S, int stype, int64_t d, int64_t lds, int k, int p,
                         int max_sweeps, float tol, float* const* V, int64_t ldv, float* const* evals,
-                        int* sweeps_out, float* resid_out, int* status_out,
-                        const deig_solver_opts* opts, void* ws, size_t ws_bytes,
-                        void* const* streams, void* stream);
+                        int* sweeps_out, float* resid_out, const deig_solver_opts* opts, void* ws,
+                        size_t ws_bytes, void* const* streams, void* stream);
 
 size_t deig_projavg_workspace(int64_t d, int64_t mk, int k, int p);
 /* With options (k > 128: block locking with the locked pairs deflated by products
@@ -311,7 +317,12 @@ int deig_oja_steps_f32(const float* X, int64_t nb, int64_t b, int64_t d, int64_t
  * read twice).  DEIG_OJA_RESIDENT: one launch per run of batches between two
  * re-orthonormalisations, each workgroup holding its block of Xb in registers (Xb
  * read once per batch); needs b = 4096, d a multiple of 512 up to 3072, k <= 32 and
- * 256 CUs (DEIG_EINVAL otherwise).  Same workspace as deig_oja_steps_f32. */
+ * 256 CUs (DEIG_EINVAL otherwise).  Its 256 workgroups wait on each other, so it is
+ * a cooperative launch: when the runtime refuses it (the grid cannot be resident at
+ * once) DEIG_OJA_RESIDENT returns DEIG_EHIP and DEIG_OJA_AUTO runs the two-pass path.
+ * If a hand-off still waits longer than 2 s (never expected), V comes back all NaN -
+ * the call is asynchronous, so NaN in V is how such a timeout is reported.  Same
+ * workspace as deig_oja_steps_f32. */
 #define DEIG_OJA_AUTO 0
 #define DEIG_OJA_TWO_PASS 1
 #define DEIG_OJA_RESIDENT 2

@@ -157,7 +157,13 @@ class _Device:
 def compute_sigma_hat(x) -> np.ndarray:
     """``SlaveNode.compute_sigma_hat_`` (distributed.py:59-70): X^T X / n, uncentered,
     as a (d, d) float64 array (bit-exactly symmetric).  Float samples go through
-    deig_syrk_shift in float64; uint8 samples through the exact deig_syrk_u8."""
+    deig_syrk_shift in float64; uint8 samples through the exact deig_syrk_u8.
+
+    uint8 input DELIBERATELY diverges from the reference: its ``np.dot(x.T, x)`` on a
+    uint8 array accumulates in uint8 and wraps modulo 256 before the float64 add
+    (distributed.py:67-69), while this returns the exact Sigma_hat of the byte values
+    (what the reference computes on the float64 grey values it actually feeds in,
+    distributed.py:169-173); ``x.astype(np.float64)`` gives the same value here."""
     _load()
     x = np.asarray(x)
     if x.ndim != 2:

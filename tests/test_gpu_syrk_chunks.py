@@ -124,3 +124,37 @@ def test_accumulate_rejects_unsupported(cuda):
         de.sigma_hat(x, accumulate=True)
     with pytest.raises(ValueError):
         de.sigma_hat(x.double(), out=S, accumulate=True)
+
+
+@pytest.mark.parametrize("d,rows", [(2048, 16384), (3072, 8192)])
+def test_full_time_to_eigenspace_helper(d, rows, cuda):
+    """bench.py's 16M-row helper (``time_to_eigenspace_16M_rows_1gpu``) at reduced
+    size: 4 row blocks regenerated in place and streamed through ONE S (block 0
+    overwrites, blocks 1-3 accumulate, each launch timed once).  S must be the
+    covariance of ALL rows (r04's helper accumulated every block twice: S = 2
+    Sigma_hat), and the top-k pairs the reference's (distributed.py:66-69 then
+    :22-29) at the north_star bars.  d = 2048 runs the fused-split kernel, d = 3072
+    the split pass."""
+    import bench
+    import distributed_eigenspaces_amd as de
+    from distributed_eigenspaces_amd import synthetic
+    k, blocks = 16, 4
+    U = synthetic.planted_basis(d, k, seed=0, device=cuda)
+    gen = bench.spiked_block_fn(synthetic, U)
+    X = torch.empty((rows, d), dtype=torch.float32, device=cuda)
+    parts = []
+    for b in range(blocks):
+        gen(b, X)
+        parts.append(X.cpu().numpy().copy())
+    Xall = np.concatenate(parts)
+    out = bench.full_time_to_eigenspace(de, gen, X, U, blocks * rows, k,
+                                        torch.cuda.current_stream(), keep_S=True)
+    assert out["blocks"] == blocks and len(out["covariance_ms_per_block"]) == blocks
+    assert out["sigma_hat_rel_err_vs_f64_sampled"] <= REL
+    assert out["evals_rel_err_vs_f64_rayleigh_all_rows"] <= 1e-5
+    Sr = ref_cpu.sigma_hat(Xall.astype(np.float64))
+    _check(out["S"].cpu().numpy(), Xall, f"16M-row helper at d={d}, {blocks} x {rows} rows", Sr)
+    w, V = ref_cpu.top_k_eigh(Sr, k)
+    ev = np.array(out["evals"])
+    assert np.max(np.abs(ev - w) / np.abs(w)) <= 1e-5
+    assert ref_cpu.projector_distance(out["V"].cpu().numpy(), V) <= 1e-4
