@@ -18,7 +18,8 @@ SOURCES = ["capi.hip", "syrk.hip", "syrk_split.hip", "syrk_u8.hip", "skinny.hip"
 # Per-source extra flags.  sweep.hip: keep the split's scalar f32 subtractions
 # unpacked (v_pk_add_f32 beside MFMAs costs issue cycles, MI355X_MICROARCH.md).
 EXTRA_FLAGS = {"sweep.hip": ["-fno-slp-vectorize"], "syrk_split.hip": ["-fno-slp-vectorize"]}
-HEADERS = ["deig_internal.hpp", os.path.join("..", "..", "include", "deig.h")]
+HEADERS = ["deig_internal.hpp", os.path.join("..", "..", "include", "deig.h"),
+           os.path.join("ab", "syrk_split_superseded.inc")]
 ARCH = os.environ.get("DEIG_OFFLOAD_ARCH", "gfx950")
 
 

@@ -19,14 +19,16 @@
 //                  [32-row block][256-feature panel][slice = (octet, hi|lo)]
 //                  [feature][8 rows] - a panel's K-tile is 32 contiguous KiB -
 //                  rows padded with zeros to a multiple of 32, + lo^2 partials;
-//   syrks_q_kernel persistent, one 512-thread block per CU, 256 x 256 lower
+//   syrks_h_kernel persistent, one 512-thread block per CU, 256 x 256 lower
 //                  tiles, v_mfma_f32_16x16x32_bf16, K-tile = 32 rows whose two
 //                  panels (32 KiB each: 4 octets x {hi, lo} x 256 features x 16 B)
 //                  are DMA'd L2/HBM -> LDS with buffer_load ... lds into two
-//                  ring buffers restaged a quarter at a time (segment_q: 4
+//                  ring buffers restaged half a K-tile at a time (segment_h: 2
 //                  phases per K-tile, waves 4-7 one barrier behind, counted
 //                  vmcnt + raw s_barrier); conflict-free ds_read_b128 reads;
-//                  (syrks_st_kernel / syrks_kernel: earlier K loops, A/B builds)
+//                  (the r02-r03 K loops syrks_st_kernel / syrks_q_kernel / the
+//                  non-fused syrks_kernel: ab/syrk_split_superseded.inc, A/B
+//                  builds only)
 //   syrks_reduce   split-K remainder tiles, summed in block order (deterministic);
 //   diag_corr      S[i][i] += alpha * sum lo_i^2.
 // Tile order: 8 x 4 super-tiles of the lower triangle, so the ~32 tiles an XCD
@@ -572,410 +574,10 @@ __device__ __forceinline__ void segment(const SSched& s, unsigned char* lds, int
   }
 }
 
-// ------------------------------------------------ staggered phases (variants 172 / 174)
-// The K-tile's work split into P phases, each an L part (this phase's ds_reads of
-// the A fragments - and the B fragments in phase 0 - plus some of the next
-// K-tile's LDS-DMA pieces) and an M part (its 96 / P MFMAs), each part closed by
-// a raw s_barrier; waves 4-7 run ONE BARRIER BEHIND waves 0-3.  Waves w and w + 4
-// share a SIMD, so between any two barriers one of them issues MFMAs while its
-// partner issues loads: the SIMD's matrix pipe stays fed instead of idling while
-// both waves issue their DMA pieces right after a common barrier (the lockstep K
-// loop above: MFMA busy 0.71, profiles/r02p_pmc_sq_tcc_syrk_c3.txt).  Same
-// 2-stage ring, same MFMA order per accumulator (bit-identical sums).
-//   RAW: the next K-tile's pieces go out in phases q < QD of this one and each wave
-//   waits for its own (vmcnt(0)) at the end of L_{P-1}, before the barrier that
-//   precedes the first read of that buffer by either group.
-//   WAR: every L part retires its reads (lgkmcnt(0)) before its closing barrier, and
-//   a buffer is restaged from the next K-tile's L_0 on - after the lagging group's
-//   last read of it (its L_{P-1} of the K-tile before) has passed that barrier.
-// KO (A/B knock-outs, measurement builds only; 0 in the shipped library): bit 0 -
-// no LDS-DMA in the K loop (every K-tile reuses the first one's LDS), bit 1 - no
-// fragment reads after the first K-tile, bit 2 - no MFMAs (operands kept live).
-template <int P, int QD, int PRIO, int KO = 0>
-__device__ __forceinline__ void segment_st(const SSched& s, unsigned char* lds, int tile,
-                                           int64_t k0, int64_t k1, int slot, bool partial,
-                                           int pace_j) {
-  static_assert(P == 2 || P == 4 || P == 8, "phases per K-tile");
-  static_assert(QD >= 1 && QD < P, "the next K-tile's pieces go out before its last phase");
-  constexpr int MBP = 8 / P;  // A blocks (16 rows) per phase
-  constexpr int BUF_B = Geo<2>::BUF_B;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wi = wave >> 2, wj = wave & 3;
-  const bool lag = wave >= 4;  // the group one barrier behind
-  const int lane16 = lane * 16;
-  const int tt = __builtin_amdgcn_readfirstlane(s.order[tile]);
-  const int ti = tt & 0xffff, tj = tt >> 16;
-  const int i0 = ti * BT, j0 = tj * BT;
-  const bool diag = (ti == tj);
-  Acc<16> acc;
-  acc.zero();
-  float* slab = partial ? s.part + (int64_t)slot * SLAB : s.accs + (int64_t)blockIdx.x * SLAB;
-  bool flushed = false;
-  const int64_t nkt = k1 - k0;
-  auto bar = [&]() {  // raw barrier; nothing moves across it
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("" ::: "memory");
-  };
-  // this wave's LDS-DMA pieces [u0, u1) of K-tile kt into buf (8 off the diagonal:
-  // slices wave*2 .. +1 of [A | B] x four 1-KiB parts; 4 on it: panel A only)
-  auto stage_part = [&](int64_t kt, unsigned char* buf, int u0, int u1) {
-    const int64_t blk = kt;  // KT = 2: one 32-row block per K-tile
-    const i32x4 rsrc = make_rsrc(s.XP + blk * (int64_t)s.nt * BLOCK_B, (uint32_t)(s.nt * BLOCK_B));
-    int l16 = lane16;
-    asm volatile("" : "+v"(l16));
-    if (!diag) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        if (i < u0 || i >= u1) continue;
-        const int c = wave * 2 + (i >> 2), p = i & 3;
-        const int pb = c / 8, sl = c % 8;
-        const int g = (pb ? j0 : i0) / BT * BLOCK_B + sl * SLICE_B;
-        dma16(rsrc, l16 + g + p * 1024, buf + pb * Geo<2>::PANEL_B + sl * SLICE_B + p * 1024);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (2 * i < u0 || 2 * i >= u1) continue;
-        const int idx = wave * 4 + i;
-        const int sl = idx >> 2, p = idx & 3;
-        dma16(rsrc, l16 + i0 / BT * BLOCK_B + sl * SLICE_B + p * 1024, buf + sl * SLICE_B + p * 1024);
-      }
-    }
-  };
-  if (nkt > 0) {
-    wait_vm<0>();     // the previous segment's stores / flushes
-    __syncthreads();  // ... and its last reads of the ring
-    stage_part(k0, lds, 0, 8);
-    wait_vm<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    bar();
-    if (lag) bar();  // the stagger
-    const int c = lane & 15, g4 = lane >> 4;
-    int since = 0, since_pace = 0;
-    const int xcd = blockIdx.x & 7;
-    const unsigned nx = (unsigned)((s.G >> 3) + (xcd < (s.G & 7) ? 1 : 0));
-    bf16x8 bhi[4], blo[4];
-    bf16x8 ahi[MBP], alo[MBP];
-    for (int64_t t = 0; t < nkt; ++t) {
-      const unsigned char* cur = lds + (t & 1) * BUF_B;
-      unsigned char* nxt = lds + ((t + 1) & 1) * BUF_B;
-      const bool more = t + 1 < nkt;
-      const unsigned char* ph = cur + ((g4 * 2) * BT + 128 * wi + c) * 16;
-      const unsigned char* qh = (diag ? cur : cur + Geo<2>::PANEL_B) + ((g4 * 2) * BT + 64 * wj + c) * 16;
-#pragma unroll
-      for (int q = 0; q < P; ++q) {
-        // ---------------- L part
-        if (q == 0) {
-          if (pace_j >= 0 && ++since_pace == s.pace_kt) {
-            since_pace = 0;
-            ++pace_j;
-            if (threadIdx.x == 0) xcd_pace(s.pace + 32 * xcd, (unsigned)pace_j * nx);
-          }
-          if (since == s.flush_kt) {  // no DMA in flight here (waited in L_{P-1})
-            flush<16>(slab, !flushed, acc, wave, lane);
-            wait_vm<0>();
-            flushed = true;
-            since = 0;
-          }
-          ++since;
-        }
-        // the next K-tile's 8 pieces over phases 0 .. QD-1 (QD = 3: 3, 3, 2)
-        if (!(KO & 1) && more && q < QD)
-          stage_part(k0 + t + 1, nxt, (8 * q + QD - 1) / QD, (8 * (q + 1) + QD - 1) / QD);
-        if (q == 0 && (!(KO & 2) || t == 0)) {
-#pragma unroll
-          for (int nb = 0; nb < 4; ++nb) {
-            bhi[nb] = *reinterpret_cast<const bf16x8*>(qh + (16 * nb) * 16);
-            blo[nb] = *reinterpret_cast<const bf16x8*>(qh + (BT + 16 * nb) * 16);
-          }
-        }
-#pragma unroll
-        for (int m = 0; m < MBP && (!(KO & 2) || t == 0); ++m) {
-          const int mb = q * MBP + m;
-          ahi[m] = *reinterpret_cast<const bf16x8*>(ph + (16 * mb) * 16);
-          alo[m] = *reinterpret_cast<const bf16x8*>(ph + (BT + 16 * mb) * 16);
-        }
-        if (more && q == P - 1) wait_vm<0>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        bar();
-        // ---------------- M part
-        if (PRIO) __builtin_amdgcn_s_setprio(1);
-        if constexpr ((KO & 4) != 0) {
-#pragma unroll
-          for (int m = 0; m < MBP; ++m) asm volatile("" ::"v"(ahi[m]), "v"(alo[m]));
-#pragma unroll
-          for (int nb = 0; nb < 4; ++nb) asm volatile("" ::"v"(bhi[nb]), "v"(blo[nb]));
-        }
-#pragma unroll
-        for (int m = 0; m < MBP && !(KO & 4); ++m) {
-          const int mb = q * MBP + m;
-#pragma unroll
-          for (int nb = 0; nb < 4; ++nb)
-            acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[m], bhi[nb], acc.a[mb][nb], 0, 0, 0);
-#pragma unroll
-          for (int nb = 0; nb < 4; ++nb)
-            acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[m], blo[nb], acc.a[mb][nb], 0, 0, 0);
-#pragma unroll
-          for (int nb = 0; nb < 4; ++nb)
-            acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[m], bhi[nb], acc.a[mb][nb], 0, 0, 0);
-        }
-        if (PRIO) __builtin_amdgcn_s_setprio(0);
-        bar();
-      }
-    }
-    if (!lag) bar();  // balance the stagger
-  }
-  if (flushed) unflush<16>(slab, acc, wave, lane);
-  if (partial) {
-#pragma unroll
-    for (int q = 0; q < NQUAD; ++q)
-      *slab_at(slab, wave, q, lane) = f32x4{acc.at(q, 0), acc.at(q, 1), acc.at(q, 2), acc.at(q, 3)};
-    return;
-  }
-#pragma unroll
-  for (int q = 0; q < NQUAD; ++q) {
-    const float a[4] = {acc.at(q, 0), acc.at(q, 1), acc.at(q, 2), acc.at(q, 3)};
-    store4(s, i0 + 128 * wi + Acc<16>::qrow(q, lane), j0 + 64 * wj + Acc<16>::qcol(q, lane), diag, a);
-  }
-}
-
-template <int P, int QD, int PRIO, int KO>
-__global__ __launch_bounds__(NTHR) void syrks_st_kernel(SSched s) {
-  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * Geo<2>::BUF_B];
-  const int L = xcd_logical(blockIdx.x, s.G);
-  // work decomposition as syrks_kernel (full phases, then K-synchronous remainder
-  // segments)
-  const int items = s.R * s.nseg;
-  const int nwork = s.q + (L < items ? (items - 1 - L) / s.G + 1 : 0);
-  for (int w = 0; w < nwork; ++w) {
-    int tile, slot = 0;
-    int64_t k0 = 0, k1 = s.NK;
-    const bool partial = w >= s.q;
-    if (!partial) {
-      tile = w * s.G + L;
-    } else {
-      const int i = L + (w - s.q) * s.G;
-      const int sg = i / s.R, r = i - sg * s.R;
-      tile = s.q * s.G + r;
-      slot = i;
-      k0 = __builtin_amdgcn_readfirstlane((int)(s.NK * sg / s.nseg));
-      k1 = __builtin_amdgcn_readfirstlane((int)(s.NK * (sg + 1) / s.nseg));
-    }
-    const int pace_j = (!partial && s.pace_kt > 0) ? (int)(w * (s.NK / s.pace_kt)) : -1;
-    segment_st<P, QD, PRIO, KO>(s, lds, tile, k0, k1, slot, partial, pace_j);
-  }
-}
-
-// ------------------------------------------------ quarter-refill ring (variants 2xxx0)
-// segment_st's phase structure (4 phases per K-tile, waves 4-7 one barrier behind,
-// an L part and an M part per phase) with the two 64-KiB ring buffers restaged at
-// quarter granularity.  Buffer = [A quarter q = 0..3: 8 slices x the 64 features
-// phase q reads (32q..32q+31 and 128+32q..+31) x 16 B][B panel: 8 slices x 256
-// features x 16 B].  Phase q of K-tile t reads A quarter q (and B in phase 0); a
-// region is restaged with K-tile t + 2 as soon as both wave groups have read it
-// (passed the barrier that closes the lagging group's L part): B and A quarter 0 in
-// L_1, quarter 1 in L_2, quarter 2 in L_3, quarter 3 in the next K-tile's L_0.  So
-// each LDS-DMA piece has ~1.5 K-tiles to land (segment_st: under one, 64 KiB in
-// flight per CU - the knock-outs put ~20 % of the K loop on that wait, profiles/
-// r03e_syrk_knockouts.log) and up to 14 pieces per wave are in flight.  Every wave
-// issues 8 pieces per K-tile (slice `wave` of each A quarter, slice `wave` of B);
-// diagonal tiles stage panel A twice (B = A) to keep the counts uniform.
-//   RAW: a wave waits (counted vmcnt) for its own pieces of a region at the end of
-//   the L part before the one that reads it, so the barrier that closes it
-//   publishes the region to both groups.  Per-wave issue order per K-tile: L_0 1
-//   (Aq3 of t+1), L_1 5 (B and Aq0 of t+2), L_2 1 (Aq1 of t+2), L_3 1 (Aq2 of t+2);
-//   hence the pieces younger than the one waited for: end of L_0 (Aq1 of t) 10,
-//   L_1 (Aq2 of t) 14, L_2 (Aq3 of t) 14, L_3 (B, Aq0 of t+1) 10.  The prologue
-//   issues K-tile 0 and then K-tile 1's B, Aq0, Aq1, Aq2 (the same order), and the
-//   last two K-tiles wait vmcnt(0).  Stores, atomics and flushes issued in between
-//   only make a counted wait stricter.
-//   WAR: every L part retires its reads (lgkmcnt(0)) before its closing barrier.
-// DS (DMA schedule): 0 - per-wave pieces per L part 1 / 5 / 1 / 1 (above); 1 - the
-// B pieces spread over L_1..L_3 (Aq0 + 2 B, Aq1 + B, Aq2 + B: 1 / 3 / 2 / 2), waits
-// 12 / 13 / 13 / 8 (prologue order Aq0 B0 B1 Aq1 B2 Aq2 B3).
-template <int PRIO, int KO = 0, int DS = 0>
-__device__ __forceinline__ void segment_q(const SSched& s, unsigned char* lds, int tile, int64_t k0,
-                                          int64_t k1, int slot, bool partial, int pace_j) {
-  constexpr int BUF_B = Geo<2>::BUF_B;
-  constexpr int QB = 8 * 1024;  // one A quarter
-  constexpr int BOFF = 4 * QB;  // the B panel
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wi = wave >> 2, wj = wave & 3;
-  const bool lag = wave >= 4;
-  const int tt = __builtin_amdgcn_readfirstlane(s.order[tile]);
-  const int ti = tt & 0xffff, tj = tt >> 16;
-  const int i0 = ti * BT, j0 = tj * BT;
-  const bool diag = (ti == tj);
-  Acc<16> acc;
-  acc.zero();
-  float* slab = partial ? s.part + (int64_t)slot * SLAB : s.accs + (int64_t)blockIdx.x * SLAB;
-  bool flushed = false;
-  const int64_t nkt = k1 - k0;
-  auto bar = [&]() {  // raw barrier; nothing moves across it
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("" ::: "memory");
-  };
-  // per-lane XP offsets inside one 32-row block: A quarter q's piece of slice
-  // `wave` (lane -> panel feature 128 (lane >> 5) + 32 q + (lane & 31)); B slice
-  // `wave`, part p (features 64 p + lane)
-  const int a_off = ti * BLOCK_B + wave * SLICE_B + ((lane >> 5) * 128 + (lane & 31)) * 16;
-  const int b_off = tj * BLOCK_B + wave * SLICE_B + lane * 16;
-  const uint32_t nrec = (uint32_t)(s.nt * BLOCK_B);
-  auto ring_rsrc = [&](int64_t kt) {
-    return make_rsrc(s.XP + kt * (int64_t)s.nt * BLOCK_B, nrec);
-  };
-  auto issue_a = [&](int64_t kt, int q, unsigned char* buf) {
-    const i32x4 r = ring_rsrc(kt);
-    int o = a_off + q * 512;
-    asm volatile("" : "+v"(o));
-    dma16(r, o, buf + q * QB + wave * 1024);
-  };
-  auto issue_b = [&](int64_t kt, unsigned char* buf, int p0 = 0, int p1 = 4) {
-    const i32x4 r = ring_rsrc(kt);
-    int o = b_off;
-    asm volatile("" : "+v"(o));
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-      if (p >= p0 && p < p1) dma16(r, o + p * 1024, buf + BOFF + wave * SLICE_B + p * 1024);
-  };
-  if (nkt > 0) {
-    wait_vm<0>();     // the previous segment's stores / flushes
-    __syncthreads();  // ... and its last reads of the ring
-    issue_b(k0, lds);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) issue_a(k0, q, lds);
-    if (nkt > 1) {
-      if constexpr (DS == 0) {
-        issue_b(k0 + 1, lds + BUF_B);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) issue_a(k0 + 1, q, lds + BUF_B);
-      } else {
-        issue_a(k0 + 1, 0, lds + BUF_B);
-        issue_b(k0 + 1, lds + BUF_B, 0, 2);
-        issue_a(k0 + 1, 1, lds + BUF_B);
-        issue_b(k0 + 1, lds + BUF_B, 2, 3);
-        issue_a(k0 + 1, 2, lds + BUF_B);
-        issue_b(k0 + 1, lds + BUF_B, 3, 4);
-      }
-      wait_vm<7>();  // K-tile k0 landed; K-tile k0 + 1's 7 pieces may fly
-    } else {
-      wait_vm<0>();
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    bar();
-    if (lag) bar();  // the stagger
-    const int c = lane & 15, g4 = lane >> 4;
-    int since = 0, since_pace = 0;
-    const int xcd = blockIdx.x & 7;
-    const unsigned nx = (unsigned)((s.G >> 3) + (xcd < (s.G & 7) ? 1 : 0));
-    bf16x8 bhi[4], blo[4];
-    bf16x8 ahi[2], alo[2];
-    for (int64_t t = 0; t < nkt; ++t) {
-      unsigned char* cur = lds + (t & 1) * BUF_B;
-      unsigned char* nxt = lds + ((t + 1) & 1) * BUF_B;
-      const bool has1 = t + 1 < nkt, has2 = t + 2 < nkt;
-      const unsigned char* pa = cur + ((g4 * 2) * 64 + 32 * wi + c) * 16;
-      const unsigned char* pb = cur + BOFF + ((g4 * 2) * BT + 64 * wj + c) * 16;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        // ---------------- L part
-        if (q == 0) {
-          if (pace_j >= 0 && ++since_pace == s.pace_kt) {
-            since_pace = 0;
-            ++pace_j;
-            if (threadIdx.x == 0) xcd_pace(s.pace + 32 * xcd, (unsigned)pace_j * nx);
-          }
-          if (since == s.flush_kt) {
-            flush<16>(slab, !flushed, acc, wave, lane);
-            wait_vm<0>();
-            flushed = true;
-            since = 0;
-          }
-          ++since;
-        }
-        if (!(KO & 1)) {
-          if (q == 0 && has1) issue_a(k0 + t + 1, 3, nxt);
-          if constexpr (DS == 0) {
-            if (q == 1 && has2) {
-              issue_b(k0 + t + 2, cur);
-              issue_a(k0 + t + 2, 0, cur);
-            }
-            if (q == 2 && has2) issue_a(k0 + t + 2, 1, cur);
-            if (q == 3 && has2) issue_a(k0 + t + 2, 2, cur);
-          } else if (has2 && q >= 1) {
-            issue_a(k0 + t + 2, q - 1, cur);
-            issue_b(k0 + t + 2, cur, q == 1 ? 0 : q, q == 1 ? 2 : q + 1);
-          }
-        }
-        if (q == 0 && (!(KO & 2) || t == 0)) {
-#pragma unroll
-          for (int nb = 0; nb < 4; ++nb) {
-            bhi[nb] = *reinterpret_cast<const bf16x8*>(pb + (16 * nb) * 16);
-            blo[nb] = *reinterpret_cast<const bf16x8*>(pb + (BT + 16 * nb) * 16);
-          }
-        }
-#pragma unroll
-        for (int m = 0; m < 2 && (!(KO & 2) || t == 0); ++m) {
-          ahi[m] = *reinterpret_cast<const bf16x8*>(pa + q * QB + (16 * m) * 16);
-          alo[m] = *reinterpret_cast<const bf16x8*>(pa + q * QB + (64 + 16 * m) * 16);
-        }
-        if (has2) {  // the younger-piece counts derived above
-          if constexpr (DS == 0) {
-            if (q == 1 || q == 2) wait_vm<14>(); else wait_vm<10>();
-          } else {
-            if (q == 1 || q == 2) wait_vm<13>(); else if (q == 0) wait_vm<12>(); else wait_vm<8>();
-          }
-        } else {
-          wait_vm<0>();
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        bar();
-        // ---------------- M part
-        if (PRIO) __builtin_amdgcn_s_setprio(1);
-        if constexpr ((KO & 4) != 0) {
-#pragma unroll
-          for (int m = 0; m < 2; ++m) asm volatile("" ::"v"(ahi[m]), "v"(alo[m]));
-#pragma unroll
-          for (int nb = 0; nb < 4; ++nb) asm volatile("" ::"v"(bhi[nb]), "v"(blo[nb]));
-        }
-#pragma unroll
-        for (int m = 0; m < 2 && !(KO & 4); ++m) {
-          const int mb = 2 * q + m;
-#pragma unroll
-          for (int nb = 0; nb < 4; ++nb)
-            acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[m], bhi[nb], acc.a[mb][nb], 0, 0, 0);
-#pragma unroll
-          for (int nb = 0; nb < 4; ++nb)
-            acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[m], blo[nb], acc.a[mb][nb], 0, 0, 0);
-#pragma unroll
-          for (int nb = 0; nb < 4; ++nb)
-            acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[m], bhi[nb], acc.a[mb][nb], 0, 0, 0);
-        }
-        if (PRIO) __builtin_amdgcn_s_setprio(0);
-        bar();
-      }
-    }
-    if (!lag) bar();  // balance the stagger
-  }
-  if (flushed) unflush<16>(slab, acc, wave, lane);
-  if (partial) {
-#pragma unroll
-    for (int q = 0; q < NQUAD; ++q)
-      *slab_at(slab, wave, q, lane) = f32x4{acc.at(q, 0), acc.at(q, 1), acc.at(q, 2), acc.at(q, 3)};
-    return;
-  }
-#pragma unroll
-  for (int q = 0; q < NQUAD; ++q) {
-    const float a[4] = {acc.at(q, 0), acc.at(q, 1), acc.at(q, 2), acc.at(q, 3)};
-    store4(s, i0 + 128 * wi + Acc<16>::qrow(q, lane), j0 + 64 * wj + Acc<16>::qcol(q, lane), diag, a);
-  }
-}
+#ifdef DEIG_AB_SYRK_VARIANT
+// the r03 K loops (staggered phases, quarter-refill ring): A/B builds only
+#include "ab/syrk_split_superseded.inc"
+#endif
 
 // Pacing points of one segment: point j (1..n) waits for the XCD counter to reach
 // base + j * mult (n = 0: none).
@@ -1230,31 +832,6 @@ __global__ __launch_bounds__(NTHR) void syrks_h_kernel(SSched s) {
       }
     }
     segment_h<PRIO>(s, lds, tile, k0, k1, slot, partial, pc);
-  }
-}
-
-template <int PRIO, int KO, int DS>
-__global__ __launch_bounds__(NTHR) void syrks_q_kernel(SSched s) {
-  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * Geo<2>::BUF_B];
-  const int L = xcd_logical(blockIdx.x, s.G);
-  const int items = s.R * s.nseg;
-  const int nwork = s.q + (L < items ? (items - 1 - L) / s.G + 1 : 0);
-  for (int w = 0; w < nwork; ++w) {
-    int tile, slot = 0;
-    int64_t k0 = 0, k1 = s.NK;
-    const bool partial = w >= s.q;
-    if (!partial) {
-      tile = w * s.G + L;
-    } else {
-      const int i = L + (w - s.q) * s.G;
-      const int sg = i / s.R, r = i - sg * s.R;
-      tile = s.q * s.G + r;
-      slot = i;
-      k0 = __builtin_amdgcn_readfirstlane((int)(s.NK * sg / s.nseg));
-      k1 = __builtin_amdgcn_readfirstlane((int)(s.NK * (sg + 1) / s.nseg));
-    }
-    const int pace_j = (!partial && s.pace_kt > 0) ? (int)(w * (s.NK / s.pace_kt)) : -1;
-    segment_q<PRIO, KO, DS>(s, lds, tile, k0, k1, slot, partial, pace_j);
   }
 }
 
@@ -1561,7 +1138,9 @@ template <int V>
 void launch_split_pass_kernel(int G, hipStream_t stream, const SSched& s) {
   if constexpr (V % 100000 >= 30000) {
     hipLaunchKernelGGL((syrks_h_kernel<(V / 10) % 10>), dim3(G), dim3(NTHR), 0, stream, s);
-  } else if constexpr (V % 100000 >= 20000) {
+  }
+#ifdef DEIG_AB_SYRK_VARIANT
+  else if constexpr (V % 100000 >= 20000) {
     hipLaunchKernelGGL((syrks_q_kernel<(V / 10) % 10, V / 100000, (V / 100) % 10>), dim3(G), dim3(NTHR), 0,
                        stream, s);
   } else if constexpr (V >= 10000) {
@@ -1574,6 +1153,11 @@ void launch_split_pass_kernel(int G, hipStream_t stream, const SSched& s) {
   } else {
     hipLaunchKernelGGL((syrks_kernel<16, 2, 2, false>), dim3(G), dim3(NTHR), 0, stream, s);
   }
+#else
+  else {
+    static_assert(V % 100000 >= 30000, "the shipped library has only the half-refill ring");
+  }
+#endif
 }
 
 }  // namespace
