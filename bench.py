@@ -98,6 +98,34 @@ def blas_cores():
         return os.cpu_count()
 
 
+def blas_max_threads() -> int:
+    """The smallest compiled thread limit (MAX_THREADS) of the OpenBLAS libraries
+    numpy / scipy load (64 if it cannot be read)."""
+    import ctypes
+    import re
+    lim = []
+    try:
+        import scipy.linalg  # noqa: F401
+        from threadpoolctl import threadpool_info
+        for i in threadpool_info():
+            if i.get("internal_api") != "openblas":
+                continue
+            lib = ctypes.CDLL(i["filepath"])
+            for fn in ("openblas_get_config", "openblas_get_config64_", "scipy_openblas_get_config64_",
+                       "scipy_openblas_get_config"):
+                f = getattr(lib, fn, None)
+                if f is None:
+                    continue
+                f.restype = ctypes.c_char_p
+                m = re.search(rb"MAX_THREADS=(\d+)", f() or b"")
+                if m:
+                    lim.append(int(m.group(1)))
+                break
+    except Exception:  # pragma: no cover
+        pass
+    return min(lim) if lim else 64
+
+
 def host_info() -> dict:
     """The host the CPU baseline ran on (nproc, CPU model,
     BLAS vendor and version): ``cores`` on a cpu_baseline is the BLAS thread count
@@ -174,6 +202,30 @@ def cpu_threaded_oneshot(xs: np.ndarray, n_total: int, k: int, m: int, cores: in
                         else "") + f" -> {t_eig:.1f}s")}
 
 
+def cpu_m1_child(xs: np.ndarray, k: int, eig_d: int, threads: int) -> dict | None:
+    """oracle/time_cpu_m1.py on ``xs`` in a child process with ``threads`` BLAS threads
+    (no GPU use in the child); None if it fails."""
+    import subprocess
+    import tempfile
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OPENBLAS_NUM_THREADS=str(threads))
+    env.pop("CUDA_VISIBLE_DEVICES", None)
+    env["HIP_VISIBLE_DEVICES"] = ""  # the child never touches the GPU
+    with tempfile.TemporaryDirectory() as tdir:
+        path = os.path.join(tdir, "sample.npy")
+        np.save(path, xs)
+        try:
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "time_cpu_m1.py"), path,
+                                str(k), str(eig_d)], env=env, capture_output=True, text=True,
+                               timeout=600)
+        except subprocess.TimeoutExpired:
+            log("cpu baseline child: timed out")
+            return None
+    if r.returncode != 0:
+        log(f"cpu baseline child failed ({r.returncode}): {r.stderr[-500:]}")
+        return None
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def cpu_baseline_oneshot(xs: np.ndarray, n_worker: int, workers: int, k: int,
                          threads: int = 8):
     """Float64 oracle (oracle/ref_cpu.py) on ``xs``, the first rows of a worker
@@ -185,23 +237,12 @@ def cpu_baseline_oneshot(xs: np.ndarray, n_worker: int, workers: int, k: int,
       the same rows (cpu_threaded_oneshot).
 
     ``value`` is the better of the two; both are reported."""
-    from threadpoolctl import threadpool_limits
     sample_rows, d = xs.shape
     cores = int(blas_cores())
+    de = min(d, EIGH_MAX_D)
 
-    def m1(nthreads):
-        """One worker on ``nthreads`` BLAS threads (None: the process default)."""
-        from oracle import ref_cpu
-        with threadpool_limits(limits=nthreads, user_api="blas"):
-            used = int(blas_cores())
-            t0 = time.perf_counter()
-            S = ref_cpu.sigma_hat(xs)
-            t_cov = time.perf_counter() - t0
-            de = min(d, EIGH_MAX_D)
-            t0 = time.perf_counter()
-            ref_cpu.top_k_eigh(S[:de, :de], k)
-            t_eig = (time.perf_counter() - t0) * (d / de) ** 3
-            del S
+    def m1_result(t_cov, t_eig, used, extra=""):
+        t_eig = t_eig * (d / de) ** 3
         t_worker = t_cov * (n_worker / sample_rows) + t_eig
         eig_note = (f"eigh top-{k} {t_eig:.2f}s" if de == d else
                     f"eigh top-{k} of the leading {de}x{de} block scaled by (d/{de})^3 -> "
@@ -211,13 +252,30 @@ def cpu_baseline_oneshot(xs: np.ndarray, n_worker: int, workers: int, k: int,
                 "note": (f"1 worker x {used} BLAS threads on {sample_rows} rows x d={d} of a "
                          f"worker shard: sigma_hat {t_cov:.2f}s + {eig_note}; covariance scaled "
                          f"linearly to {n_worker} rows -> {t_worker:.1f}s per worker shard, x "
-                         f"{workers} worker(s)")}
+                         f"{workers} worker(s){extra}")}
 
-    single = m1(None)
-    # SURVEY.md §8(d)'s "m = 1 x all cores": every CPU of the host, whatever
-    # OMP_NUM_THREADS says (16 on the GPU box); BLAS may cap the count it really uses
+    from oracle import ref_cpu
+    t0 = time.perf_counter()
+    S = ref_cpu.sigma_hat(xs)
+    t_cov = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    ref_cpu.top_k_eigh(S[:de, :de], k)
+    t_eig = time.perf_counter() - t0
+    del S
+    single = m1_result(t_cov, t_eig, cores)
+    # SURVEY.md §8(d)'s "m = 1 x all cores": every CPU of the host up to the BLAS's
+    # compiled limit (numpy / scipy's OpenBLAS: MAX_THREADS=64), in a child process
+    # whose thread count is set before numpy loads (raising it in this process with
+    # threadpool_limits crashed OpenBLAS on the 256-CPU GPU host)
     nproc = os.cpu_count() or 1
-    allc = m1(nproc) if nproc > cores else None
+    want = min(nproc, blas_max_threads())
+    allc = None
+    if want > cores:
+        allc = cpu_m1_child(xs, k, de, want)
+        if allc is not None:
+            allc = m1_result(allc["t_cov_s"], allc["t_eig_s"], allc.get("blas_threads") or want,
+                             f" (child process, OPENBLAS_NUM_THREADS={want}; host nproc {nproc}, "
+                             f"BLAS MAX_THREADS {blas_max_threads()})")
     threaded = None
     if threads > 1:
         threaded = cpu_threaded_oneshot(xs, workers * n_worker, k, threads, cores,

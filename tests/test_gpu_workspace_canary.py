@@ -20,9 +20,11 @@ CANARY = 1 << 20
 FILL = 0xA5
 
 
-def _spd(d, seed):
+def _spd(d, seed, k=16):
+    """Top-k eigenvalues 40..10 above a [0, 5) bulk: a gap at k the 1e-4 projector bar
+    can resolve at the solver's 1e-6 residual."""
     rng = np.random.default_rng(seed)
-    w = np.concatenate([np.linspace(40.0, 10.0, min(d, 16)), rng.uniform(0.0, 1.0, d - min(d, 16))])
+    w = np.concatenate([np.linspace(40.0, 10.0, min(d, k)), rng.uniform(0.0, 5.0, d - min(d, k))])
     Q, _ = np.linalg.qr(rng.standard_normal((d, d)))
     return ((Q * w) @ Q.T).astype(np.float32)
 
@@ -53,16 +55,14 @@ def _solve_with_canary(S, k, algo, cuda):
                                  (512, 64), (512, 128), (1024, 128)])
 def test_topk_stays_in_workspace(d, k, algo, cuda):
     from distributed_eigenspaces_amd import _lib
-    A = _spd(d, seed=d + k)
+    A = _spd(d, seed=d + k, k=k)
     S = torch.from_numpy(A).to(cuda)
     V, ev, bad = _solve_with_canary(S, k, _lib.SWEEP_ALGOS[algo], cuda)
     assert bad == 0, f"d={d} k={k} {algo}: {bad} canary bytes overwritten past the workspace"
     w, Vr = ref_cpu.top_k_eigh(A.astype(np.float64), k)
-    assert np.max(np.abs(ev - w) / np.abs(w).max()) <= 1e-5
+    assert np.max(np.abs(ev - w) / np.abs(w)) <= 1e-5
     if k < d:  # k = d: every direction, the projector is the identity either way
-        gap_ok = (w[0] - (np.linalg.eigvalsh(A.astype(np.float64))[-k - 1])) > 1e-3
-        if gap_ok:
-            assert ref_cpu.projector_distance(V, Vr) <= 1e-4
+        assert ref_cpu.projector_distance(V, Vr) <= 1e-4
 
 
 @pytest.mark.parametrize("d,k", [(128, 64), (256, 128), (512, 32)])
@@ -74,7 +74,7 @@ def test_batch_stays_in_workspace(d, k, cuda):
     from distributed_eigenspaces_amd import _lib
     L = _lib.lib()
     W = 4
-    mats = [torch.from_numpy(_spd(d, seed=100 * i + d)).to(cuda) for i in range(W)]
+    mats = [torch.from_numpy(_spd(d, seed=100 * i + d, k=k)).to(cuda) for i in range(W)]
     o = _lib.solver_opts()
     nbytes = L.deig_topk_batch_workspace(W, d, k, 0, _lib.DEIG_F32, ctypes.byref(o))
     buf = torch.full((nbytes + CANARY,), FILL, dtype=torch.uint8, device=cuda)
