@@ -94,14 +94,15 @@ def test_c4_oja_config_shape_vs_oracle(cuda):
     orth_every; parity unpinned (no Oja in the reference): ref_cpu.oja_epoch."""
     import distributed_eigenspaces_amd as de
     from distributed_eigenspaces_amd import synthetic
-    b, d, k, nb, eta = 4096, 3072, 32, 16, 0.02
+    import bench
+    b, d, k, nb, eta = 4096, 3072, 32, 32, 0.02
     U = synthetic.planted_basis(d, k, seed=0, device=cuda)
     X = synthetic.spiked_samples(nb * b, U, seed=3)
     g = torch.Generator(device="cpu").manual_seed(5)
     V0 = torch.linalg.qr(torch.randn(d, k, generator=g, dtype=torch.float64))[0]
     Vr = ref_cpu.oja_epoch(X.double().cpu().numpy(), V0.numpy(), eta, b)
     V = V0.float().to(cuda).t().contiguous().t()
-    de.oja_steps(X, V, eta, b, orth_every=8)
+    de.oja_steps(X, V, eta, b, orth_every=bench.CONFIGS["c4"]["orth_every"])
     Vg = V.cpu().numpy()
     np.testing.assert_allclose(Vg.T @ Vg, np.eye(k), atol=1e-5)
     assert ref_cpu.projector_distance(Vg, Vr) <= P_TOL
