@@ -728,7 +728,11 @@ int sweep_ks(int64_t d) {
 // sweep no gain either).  Ring depths 5-8 measured the same as 3
 // (profiles/r02n_sweep_mb.log), so the ring is 3 deep.
 int sweep_mb(bool pre, int nb) { return (pre && nb <= 5) ? 2 : 4; }
+#ifdef DEIG_AB_SWEEP_DEPTH
+constexpr int kSweepDepth = DEIG_AB_SWEEP_DEPTH;
+#else
 constexpr int kSweepDepth = 3;
+#endif
 
 // Split-K slices of a v3 launch with mb m-blocks per wave (rows per block 64 mb).
 int sweep_ks_mb(int64_t d, int mb) {
