@@ -547,7 +547,8 @@ __global__ __launch_bounds__(512) void oja_tn_kernel(const float* __restrict__ X
 // write-through (sc1) and drained (vmcnt(0), then the workgroup barrier), ONE lane adds
 // to the group's counter, ONE lane polls it (relaxed agent loads), the payload is
 // read with sc1 loads only.  Column group j lives on one XCD (its C / D hand-offs stay
-// in that L2); row groups span all eight.  Counters are zeroed per launch and every
+// in that L2); row groups span all eight.  Counters start each launch at zero (the
+// last block out resets them) and every
 // spin is bounded (2 s): a timeout sets *err, every later wait returns at once, and
 // the final copy-out poisons V with NaN - a failure is loud, never a hang.
 constexpr int OB_G = 256, OB_NR = 16, OB_NF = 16, OB_RB = 256, OB_TS = 36;
@@ -564,7 +565,7 @@ struct OjaBlk {
   u32x4* timg;     // T's image (TN B operand)
   float* ppart;    // [16 j][b / 4][kp][4]
   float* qpart;    // [16 i][d / 4][kp][4]
-  unsigned* cnt;   // [4 phases][16 groups] x OB_CNT_LINE
+  unsigned* cnt;   // [4 phases][16 groups] x OB_CNT_LINE, then the exit count
   unsigned* err;
   unsigned long long* trace;  // measurement builds only (DEIG_AB_OJA_TRACE)
 };
@@ -858,17 +859,35 @@ __global__ __launch_bounds__(512) void oja_blk_kernel(OjaBlk a) {
     }
     OB_STAMP(9, t == 0);
   }
+#ifndef DEIG_AB_OJA_COOP
+  // The hand-off counters are left at zero for the next launch on this workspace
+  // (no memset and its kernel boundary between runs): every block drains its own
+  // counter atomics (vmcnt(0): performed, not just issued), then counts itself out;
+  // the last one out - every other block is past all of its waits and signals -
+  // zeroes the counters and the exit count.
+  ob_drain();
+  __syncthreads();
+  if (t == 0) {
+    unsigned* ce = a.cnt + 4 * 16 * OB_CNT_LINE;
+    if (__hip_atomic_fetch_add(ce, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == OB_G - 1u) {
+      for (int c = 0; c < 4 * 16; ++c)
+        __hip_atomic_store(a.cnt + c * OB_CNT_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ce, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+#endif
 }
 
 struct OjaWs {
-  unsigned *cnt, *err;  // v4 hand-off counters (zeroed per launch) and timeout word
+  unsigned *cnt, *err;  // v4 hand-off counters (zero between launches) and timeout word
   float *Vr, *Vr2, *G, *Rinv, *slab;
   u32x4 *vimg, *timg;  // bf16 operand images of V (NN) and T (TN)
   float *ppart, *qpart;  // v4 partials
   unsigned long long* trace;
   size_t slab_bytes;
 };
-constexpr size_t OB_CNT_BYTES = 4 * 16 * OB_CNT_LINE * sizeof(unsigned);
+// [4 phases][16 groups] hand-off counters + the exit count, one per 128-B line
+constexpr size_t OB_CNT_BYTES = (4 * 16 + 1) * OB_CNT_LINE * sizeof(unsigned);
 
 OjaWs carve_oja(void* ws, size_t cap, int64_t b, int64_t d, int kp, size_t* total) {
   Carve c(ws, cap);
@@ -963,10 +982,42 @@ bool oja_blk_eligible(int64_t b, int64_t d, int64_t ldx, int kp) {
 }
 
 // The resident kernel's workgroups wait on each other, so all OB_G of them must be
-// resident at once: a cooperative launch, which the runtime refuses (instead of
-// starting a grid that could deadlock until the 2-s spin bound) when they cannot be.
+// resident at once.  r05 measured the cooperative launch (hipLaunchCooperativeKernel)
+// at ~12 us of idle device time on each side of every run (profiles/r05p_c4_*): it
+// drains the queue first.  Its only service is the launch-time check of the grid
+// against the occupancy query (MI355X_MICROARCH.md, cost table 'coop-launch'), so the
+// same check is made here once per kernel instance - one workgroup of 512 threads per
+// CU on >= OB_G CUs - and the grid goes out as a plain launch.  A device whose CUs are
+// held by other work can still delay some workgroups: the 2-s spin bound turns that
+// into NaN output (see above), never a hang.
+template <int NB, int NKS>
+bool oja_blk_fits() {
+  static const bool ok = [] {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, oja_blk_kernel<NB, NKS>, 512, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return n >= 1 && num_cus() >= OB_G;
+  }();
+  return ok;
+}
+
 template <int NB>
 hipError_t launch_oja_blk(int nks, const OjaBlk& a, hipStream_t st) {
+#ifndef DEIG_AB_OJA_COOP
+  switch (nks) {
+#define DEIG_OJA_NKS(x)                                                                         \
+  case x:                                                                                       \
+    if (!oja_blk_fits<NB, x>()) return hipErrorCooperativeLaunchTooLarge;                      \
+    hipLaunchKernelGGL((oja_blk_kernel<NB, x>), dim3(OB_G), dim3(512), 0, st, a);               \
+    return hipGetLastError();
+    DEIG_OJA_NKS(1) DEIG_OJA_NKS(2) DEIG_OJA_NKS(3) DEIG_OJA_NKS(4) DEIG_OJA_NKS(5) DEIG_OJA_NKS(6)
+#undef DEIG_OJA_NKS
+    default:
+      return hipErrorInvalidValue;
+  }
+#else
   const void* fn = nullptr;
   switch (nks) {
 #define DEIG_OJA_NKS(x) \
@@ -981,6 +1032,7 @@ hipError_t launch_oja_blk(int nks, const OjaBlk& a, hipStream_t st) {
   OjaBlk arg = a;
   void* args[] = {&arg};
   return hipLaunchCooperativeKernel(fn, dim3(OB_G), dim3(512), args, 0, st);
+#endif
 }
 
 int oja_steps_launch(const float* X, int64_t nb, int64_t b, int64_t d, int64_t ldx, float eta,
@@ -1026,7 +1078,12 @@ int oja_steps_launch(const float* X, int64_t nb, int64_t b, int64_t d, int64_t l
   for (int64_t i0 = 0; i0 < nb;) {
     const int64_t i1 = std::min(nb, (i0 / orth_every + 1) * orth_every);
     if (blk) {
+#ifndef DEIG_AB_OJA_COOP
+      // zeroed once per call: each launch leaves them at zero for the next
+      if (i0 == 0) DEIG_HIP_CHECK(hipMemsetAsync(o.cnt, 0, OB_CNT_BYTES, st));
+#else
       DEIG_HIP_CHECK(hipMemsetAsync(o.cnt, 0, OB_CNT_BYTES, st));
+#endif
       OjaBlk a;
       a.X = X + i0 * b * ldx;
       a.ldx = ldx;
@@ -1051,7 +1108,7 @@ int oja_steps_launch(const float* X, int64_t nb, int64_t b, int64_t d, int64_t l
         // device): DEIG_OJA_RESIDENT reports it, AUTO runs this and every later run
         // on the two-pass kernels (the same arithmetic, to within 1e-5)
         if (algo == DEIG_OJA_RESIDENT)
-          return fail(DEIG_EHIP, "oja: cooperative launch of the resident kernel refused: %s",
+          return fail(DEIG_EHIP, "oja: the resident kernel's grid cannot be co-resident: %s",
                       hipGetErrorString(le));
         blk = false;
       }

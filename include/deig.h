@@ -317,10 +317,11 @@ int deig_oja_steps_f32(const float* X, int64_t nb, int64_t b, int64_t d, int64_t
  * read twice).  DEIG_OJA_RESIDENT: one launch per run of batches between two
  * re-orthonormalisations, each workgroup holding its block of Xb in registers (Xb
  * read once per batch); needs b = 4096, d a multiple of 512 up to 3072, k <= 32 and
- * 256 CUs (DEIG_EINVAL otherwise).  Its 256 workgroups wait on each other, so it is
- * a cooperative launch: when the runtime refuses it (the grid cannot be resident at
- * once) DEIG_OJA_RESIDENT returns DEIG_EHIP and DEIG_OJA_AUTO runs the two-pass path.
- * If a hand-off still waits longer than 2 s (never expected), V comes back all NaN -
+ * 256 CUs (DEIG_EINVAL otherwise).  Its 256 workgroups wait on each other, so the
+ * grid is checked against the occupancy query (one 512-thread workgroup per CU on
+ * >= 256 CUs) before its plain launch: when it does not fit, DEIG_OJA_RESIDENT
+ * returns DEIG_EHIP and DEIG_OJA_AUTO runs the two-pass path.  If a hand-off still
+ * waits longer than 2 s (CUs held by other persistent work), V comes back all NaN -
  * the call is asynchronous, so NaN in V is how such a timeout is reported.  Same
  * workspace as deig_oja_steps_f32. */
 #define DEIG_OJA_AUTO 0

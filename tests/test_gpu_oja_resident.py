@@ -77,3 +77,32 @@ def test_resident_refuses_other_shapes(cuda):
         de.oja_steps(X, V, 0.02, 2048, algo="resident")
     de.oja_steps(X, V, 0.02, 2048, algo="auto")  # auto takes the two-pass path there
     assert torch.isfinite(V).all()
+
+
+def test_resident_counters_reset_between_launches(cuda):
+    """Each resident launch leaves its hand-off counters at zero for the next one (the
+    last workgroup out resets them; only the call's first launch is preceded by a
+    memset): 12 launches per call (orth_every = 1), three calls on one workspace with
+    no re-initialisation between them - bit-identical results, every counter line (the
+    first 65 x 128 B of the workspace) zero after each call."""
+    from distributed_eigenspaces_amd import _lib
+    b, d, k, nb, eta = 4096, 1024, 16, 12, 0.02
+    X, V0 = _data(nb, b, d, k, seed=23)
+    L = _lib.lib()
+    nbytes = L.deig_oja_workspace(b, d, k)
+    ws = torch.full((nbytes // 4 + 1,), float("nan"), dtype=torch.float32, device=X.device)
+    outs = []
+    for _ in range(3):
+        V = V0.float().to(X.device).t().contiguous().t()
+        rc = L.deig_oja_steps_ex(X.data_ptr(), nb, b, d, X.stride(0), ctypes.c_float(eta),
+                                 V.data_ptr(), k, V.stride(1), 1, _lib.DEIG_OJA_RESIDENT,
+                                 ws.data_ptr(), nbytes, None)
+        assert rc == _lib.DEIG_OK, _lib.last_error()
+        torch.cuda.synchronize()
+        outs.append(V.cpu().numpy())
+        cnt = ws[:65 * 32].view(torch.int32).cpu().numpy()
+        assert not cnt.any(), f"counter lines left non-zero: {np.flatnonzero(cnt)[:8]}"
+    assert np.isfinite(outs[0]).all()
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[1], outs[2])
+    Vt = _run(X, V0, eta, b, 1, "two_pass")
+    assert ref_cpu.projector_distance(outs[0].astype(np.float64), Vt) <= 1e-5
