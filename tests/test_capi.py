@@ -124,8 +124,9 @@ def test_library_reads_no_environment():
     import shutil
     import subprocess
     csrc = os.path.join(os.path.dirname(_lib.HERE), "distributed_eigenspaces_amd", "csrc")
-    for f in os.listdir(csrc):
-        assert "getenv" not in open(os.path.join(csrc, f)).read(), f
+    for root, _, files in os.walk(csrc):  # csrc/ab/ holds the A/B-only sources
+        for f in files:
+            assert "getenv" not in open(os.path.join(root, f)).read(), os.path.join(root, f)
     nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
     if os.path.exists(nm):
         out = subprocess.run([nm, "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True,
