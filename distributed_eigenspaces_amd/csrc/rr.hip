@@ -823,6 +823,10 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
         break;
       }
     }
+    // wave 0, lane t < half: the round-robin pair of step st, a = (st + t) mod (p - 1),
+    // b = (st - t) mod (p - 1) (lane 0: a = p - 1, b = st), advanced by one per step
+    int pa = tid == 0 ? p - 1 : tid, pb = tid == 0 ? 0 : p - 1 - tid;
+    int swsum = 0;  // wave 0: this sweep's rotations
     for (int st = 0; st < p - 1; ++st) {
       const int ci = 1 + (st & 1);
 #ifdef DEIG_AB_RR_JOLD
@@ -849,14 +853,9 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
       if (wave == 0) {
         bool rot = false;
         if (tid < half) {
-          int a, b;
-          if (tid == 0) {
-            a = p - 1;
-            b = st;
-          } else {
-            a = (st + tid) % (p - 1);
-            b = (st - tid + (p - 1)) % (p - 1);
-          }
+          const int a = pa, b = pb;
+          if (tid != 0) pa = pa + 1 == p - 1 ? 0 : pa + 1;
+          pb = pb + 1 == p - 1 ? 0 : pb + 1;
           const float app = X1[a * p + a], aqq = X1[b * p + b], apq = X1[a * p + b];
           float c = 1.f, s = 0.f;
           if (fabsf(apq) > abs_thr && fabsf(apq) > jrel * __builtin_amdgcn_sqrtf(fabsf(app * aqq))) {
@@ -867,6 +866,7 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
         }
         const int cnt = __popcll(__ballot(rot));
         if (tid == 0) nrot[ci] = cnt;
+        swsum += cnt;
       }
 #endif
       __syncthreads();
@@ -941,11 +941,16 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
 #endif
       }
       __syncthreads();
+#ifdef DEIG_AB_RR_JOLD
       if (tid == 0) {
         nrot[0] += step_rot;
         nrot[ci] = 0;
       }
+#endif
     }
+#ifndef DEIG_AB_RR_JOLD
+    if (tid == 0) nrot[0] = swsum;
+#endif
     __syncthreads();
     const int swrot = nrot[0];
     if (tid == 0) {
