@@ -989,8 +989,8 @@ def run_oja(args, cfg, world, rank, dev):
         "parallelism": f"dp{world} (one Oja stream per GPU; RCCL all-gather + broadcast of "
                        f"bases every {agg} batches)"})
     resident = b == 4096 and d % 512 == 0 and d <= 3072 and k <= 32  # DEIG_OJA_AUTO's choice
-    kname = ("Oja steps (oja_blk_kernel: one cooperative launch per run of orth_every batches, Xb "
-             "held in registers "
+    kname = ("Oja steps (oja_blk_kernel: one launch per run of orth_every batches, its 256 "
+             "workgroups co-resident (occupancy-checked), Xb held in registers "
              "and read from HBM once per batch, Xb*V and Xb^T*T as bf16x3 split products, "
              "in-launch hand-offs; CholQR every orth_every batches), whole op per batch" if resident else
              "Oja steps (oja_nn_kernel Xb*V + oja_tn_kernel V += c Xb^T*T, bf16x3 split "
