@@ -88,7 +88,7 @@ struct Opts {
   int sweep_algo = DEIG_SWEEP_BF16X6;
   int rr_every = 0;
   bool cheb = true;
-  float cheb_above = 1e-2f;
+  float cheb_above = -1.f;  // < 0: per solve (Solver::iter_begin)
   bool deflate = true;
   bool deflate_early = true;
   int jcap_sweeps = -1;
@@ -282,9 +282,10 @@ int apply_op(const Operator& op, const SolverWs& w, int64_t d, int p, hipStream_
 // column's contamination by theta_0's direction grows at most gmax = clamp(1/resid,
 // 10, kChebGmax) times (the fp32 Gram of the filtered block must still resolve
 // every column); columns whose growth would exceed gmax stay out of the filter
-// (threshold thr on theta_j).  Only used once resid <= cheb_above: before that the
-// Ritz values are too rough to place the interval, and plain power steps run.
-// cheb_above stays 1e-2 (r04 A/B, profiles/r04k_solver_opts_sweep.log and r04m_*): 0.1
+// (threshold thr on theta_j).  Only used once resid <= cheb_above (Solver::iter_begin:
+// 1.0 - from the first RR on - for single-block explicit solves since r05, else 1e-2):
+// before that plain power steps run.  r04 kept 1e-2 everywhere (r04 A/B,
+// profiles/r04k_solver_opts_sweep.log and r04m_*): 0.1
 // cut synthetic worker solves 6-16 % (c5 18.0 -> 16.6 ms at the same bars) but the c1
 // bench's uncentered byte covariances took 31-37 sweeps instead of 28-29 (c1 8.06 ->
 // 7.0 M samples/s: the dominant direction holds an early filter to degree 1), and 0.5
@@ -407,7 +408,7 @@ struct Solver {
   float* evb = nullptr;
   bool allow_early = false, early = false;
   int rr_every = 4, jcap_sweeps = 2, jcap = 30, nrr = 0, start = 0, since_best = 0;
-  float tau = 0.f, jcap_above = 1e-4f, best = 3.4e38f;
+  float tau = 0.f, jcap_above = 1e-4f, best = 3.4e38f, cheb_above = 1e-2f;
   // |theta| scale of the whole operator (the first block's Ritz values; 0 until the
   // first block has ended) and the factor that turns the last RR's residuals from
   // "relative to the block's own largest Ritz value" (rr_finish_kernel) into
@@ -441,7 +442,8 @@ struct Solver {
   // columns beyond k (measured: d=8192 k=64 p=80 6.2 vs 9.0 ms, d=3072 k=16 p=32 1.4
   // vs 1.9 ms); every 2nd without them (d=16384 k=128 p=128: 23 sweeps / 47 ms vs
   // 41 / 54 ms).
-  void iter_begin(int kc_, int pb_, float* Vb_, int64_t ldv_, float* evb_, bool allow_early_) {
+  void iter_begin(int kc_, int pb_, float* Vb_, int64_t ldv_, float* evb_, bool allow_early_,
+                  bool single_block) {
     kc = kc_;
     pb = pb_;
     Vb = Vb_;
@@ -462,6 +464,18 @@ struct Solver {
     // step is the exact eigendecomposition - run its Jacobi to convergence
     if (pb >= d) jcap_sweeps = 0;
     jcap_above = o.jcap_above >= 0.f ? o.jcap_above : (op.implicit ? 1e-2f : 1e-4f);
+    // The Chebyshev filter from the first Rayleigh-Ritz step on for a single-block
+    // solve of an explicit S on a basis without guard columns (p - k < 4: the filter's
+    // interval ends at theta_k / 2, which holds from the first RR on), else once resid
+    // <= 1e-2 (r05, tools/solver_opts_sweep.py and tools/cheb_policy_ab.py,
+    // profiles/r05w_*: config-5 worker 14.5 -> 11.9 ms, the p = k test spectrum 6.87 ->
+    // 6.18 ms, same bars; with guard columns the early interval ends at an unconverged
+    // guard Ritz value: config-3 shard 3.10 -> 3.05 ms but the spiked d = 3072 test
+    // 13 -> 14 sweeps, 0.857 -> 0.884 ms; block locking, k > 128, stalled above the
+    // accept floor with the early filter, as in r04; the implicit projector averages
+    // are clustered near 1).
+    cheb_above = o.cheb_above >= 0.f ? o.cheb_above
+                                     : ((single_block && !op.implicit && pb - kc < 4) ? 1.0f : 1e-2f);
     fuse = w.sweep_ws != nullptr;
     best = 3.4e38f;
     since_best = 0;
@@ -513,7 +527,7 @@ struct Solver {
                       : last > fmaxf(o.round_until, tol)                      ? kSweepRoundQ
                                                                               : kSweepExact;
     ChebPlan cp;
-    const bool cheb = o.cheb && nrr > 0 && cheb_plan(lam_h, kc, pb, last, tol, o.cheb_above, &cp);
+    const bool cheb = o.cheb && nrr > 0 && cheb_plan(lam_h, kc, pb, last, tol, cheb_above, &cp);
     int nstep = 0;
     ncheb_dbg = 0;
     SweepStep step{};
@@ -949,7 +963,7 @@ struct SolveSM {
       r = rr_init_launch(sv.w.rr.Z, d, pb, nullptr, 0, 0, 0x5eed5eedull + locked, sv.st, valid);
     }
     if (r) return r;
-    sv.iter_begin(kc, pb, Vb, ldv, evb, can_deflate && sv.o.deflate_early && !redo);
+    sv.iter_begin(kc, pb, Vb, ldv, evb, can_deflate && sv.o.deflate_early && !redo, k <= kMaxP);
     state = CYCLE;
     return DEIG_OK;
   }
@@ -1303,7 +1317,7 @@ void deig_solver_opts_init(deig_solver_opts* o) {
   o->sweep_algo = DEIG_SWEEP_AUTO;
   o->rr_every = 0;
   o->chebyshev = 1;
-  o->cheb_above = 1e-2f;
+  o->cheb_above = -1.f;
   o->deflate = 1;
   o->deflate_early = 1;
   o->jacobi_early_sweeps = -1;

@@ -189,7 +189,9 @@ typedef struct deig_solver_opts {
   int rr_every;              /* sweeps per Rayleigh-Ritz step before the Chebyshev filter
                                 starts (0: 4 with >= 16 guard columns, else 2) */
   int chebyshev;             /* 1 (default): Chebyshev filter once resid <= cheb_above */
-  float cheb_above;          /* 1e-2 */
+  float cheb_above;          /* < 0 (default): 1.0 - the filter from the first Rayleigh-Ritz
+                                step on - for a single-block solve of an explicit S (k <= 128)
+                                on a basis without guard columns (p - k < 4), else 1e-2 */
   int deflate;               /* 1 (default): lock dominant pairs (theta_1 >= 64 theta_k) and
                                 iterate the rest on the deflated operator */
   int deflate_early;         /* 1 (default): lock them as soon as they are converged */

@@ -107,7 +107,7 @@ def test_solver_opts_struct_and_defaults():
     o = _lib.solver_opts()
     assert o.size == ctypes.sizeof(_lib.SolverOpts)
     assert (o.chebyshev, o.deflate, o.deflate_early, o.rr_every) == (1, 1, 1, 0)
-    assert abs(o.cheb_above - 1e-2) < 1e-9 and abs(o.fast_until - 1e-3) < 1e-9
+    assert o.cheb_above < 0 and abs(o.fast_until - 1e-3) < 1e-9  # cheb_above: per solve
     assert abs(o.round_until - 1e-4) < 1e-9 and o.jacobi_early_sweeps == -1
     bad = _lib.SolverOpts()
     bad.size = 4
