@@ -1211,12 +1211,21 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
 
   // Two-level fp32 summation: accumulators are added into a per-block slab every
   // flush_rows rows.  The error bound ~ (flush_rows / 32 + n / flush_rows) eps is
-  // smallest at flush_rows ~ sqrt(32 n): 2^floor(log2 sqrt(32 n)) within [4096, 16384]
-  // (config 3, n = 2^21: 8192 - vs 4096 the op ran 337.6 -> 331.1 ms with sampled
-  // error 5.0e-7 -> 4.7e-7, profiles/r02l_syrk_flush.log; fewer flushes, each a
-  // read-add-write of the block's 256 KiB slab beside stalled MFMAs).
+  // smallest at flush_rows ~ sqrt(32 n); each flush is a read-add-write of the block's
+  // 256 KiB slab beside stalled MFMAs, and the measured error grows slowly above that
+  // point, so the rule is 2^floor(log2 sqrt(128 n)) within [4096, 16384] (r05,
+  // interleaved A/B with a float64 check of 64 sampled columns, tools/syrk_lib_ab.py,
+  // profiles/r05z_syrk_flush_ab.log: config-3 shard 8192 -> 16384 rows 314.2 -> 308.6
+  // ms, max error / max|S| 7.0e-7 -> 8.0e-7; config 2 4096 -> 8192 26.58 -> 25.78 ms,
+  // 1.9e-7 -> 4.2e-7; 32768 rows at config 3: 305.8 ms but 1.4e-6, config 5's
+  // n = 65536 at 16384: 2.0e-6 - not taken; r02: 4096 -> 8192 at config 3 337.6 ->
+  // 331.1 ms, profiles/r02l_syrk_flush.log).
+#ifdef DEIG_AB_SYRK_FLUSH_ROWS
+  int64_t flush_rows = DEIG_AB_SYRK_FLUSH_ROWS;
+#else
   int64_t flush_rows = 4096;
-  while (flush_rows < 16384 && (flush_rows * 2) * (flush_rows * 2) <= 32 * n) flush_rows *= 2;
+  while (flush_rows < 16384 && (flush_rows * 2) * (flush_rows * 2) <= 128 * n) flush_rows *= 2;
+#endif
   s.prio = 0;  // s_setprio staggering measured slower (374 vs 342 ms, r02)
   s.pace = reinterpret_cast<unsigned*>(base + L.off_pace);
   // XCD pacing every 64 K-tiles (2048 rows): config 3 L2 hit rate 0.52 -> 0.75, fabric
