@@ -103,6 +103,19 @@ struct SSched {
 // arrived.  Relaxed atomics, no fence: nothing is published, so no L2 write-back.
 // The result's wait (vmcnt(0)) also drains this wave's ring DMAs, which keeps the
 // counted vmcnt waits exact.
+// Chip-wide pacing (r05): in the full-tile phases every kChipPaceEvery-th XCD pacing
+// point also waits for all G blocks on one more counter (same bounded spin), which
+// keeps the eight XCDs within ~128 K-tiles (~128 MB of the XP image) of each other,
+// so a panel's K-tile fetched from HBM by one XCD is still in the Infinity Cache when
+// the other XCDs that use the panel read it.  Interleaved A/B at config 3 (one
+// process, bit-identical, profiles/r05zb_syrk_chip_pacing_ab.log): 296.6 -> 283.7 ms
+// per op at every 2nd point; every point 286.0, every 3rd 286.5, every 4th 294.0;
+// chip-wide only (no XCD level) 292.5; XCD pacing off 327.8.  Remainder rounds with
+// global item numbering are chip-paced too, against the round's item count (config 2,
+// all remainder: 24.77 -> 24.54 ms; config 3 286.0 -> 284.8).  Config 5 (short K per
+// tile) is unchanged.
+constexpr int kChipPaceEvery = 2;
+
 __device__ __noinline__ void xcd_pace(unsigned* ctr, unsigned target) {
   __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t t0 = wall_clock64();
@@ -584,6 +597,9 @@ __device__ __forceinline__ void segment(const SSched& s, unsigned char* lds, int
 struct PaceSeq {
   int n;
   unsigned base, mult;
+  unsigned gbase = 0;  // the chip-wide counter's target before this segment
+  unsigned gmult = 0;  // blocks that pace chip-wide with this one (G, or a round's items)
+  bool g = false;      // every kChipPaceEvery-th point is also chip-wide
 };
 
 // Blocks of this block's XCD (logical L) that run a remainder item in round u.
@@ -712,6 +728,8 @@ __device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, i
     int since = 0, since_pace = 0, pace_left = pc.n;
     unsigned pace_t = pc.base;
     const int xcd = blockIdx.x & 7;
+    int gcount = 0;
+    unsigned gtarget = pc.gbase;
     bf16x8 bhi[4], blo[4];
     bf16x8 ahi[4], alo[4];
     for (int64_t t = 0; t < nkt; ++t) {
@@ -729,6 +747,11 @@ __device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, i
             --pace_left;
             pace_t += pc.mult;
             if (threadIdx.x == 0) xcd_pace(s.pace + 32 * xcd, pace_t);
+            if (pc.g && ++gcount == kChipPaceEvery) {  // ... and every other one chip-wide
+              gcount = 0;
+              gtarget += pc.gmult;
+              if (threadIdx.x == 0) xcd_pace(s.pace + 32 * 8, gtarget);
+            }
           }
           if (since == s.flush_kt) {
             flush<16>(slab, !flushed, acc, wave, lane);
@@ -821,6 +844,9 @@ __global__ __launch_bounds__(NTHR) void syrks_h_kernel(SSched s) {
     if (!partial) {
       tile = w * s.G + L;
       pc = PaceSeq{(int)P, (unsigned)w * P * nx, nx};
+      pc.g = true;
+      pc.gbase = (unsigned)w * (P / kChipPaceEvery) * (unsigned)s.G;
+      pc.gmult = (unsigned)s.G;
     } else {
       rem_item(s, L, w - s.q, tile, slot, sg);
       k0 = __builtin_amdgcn_readfirstlane((int)(s.NK * sg / s.nseg));
@@ -829,6 +855,17 @@ __global__ __launch_bounds__(NTHR) void syrks_h_kernel(SSched s) {
         unsigned before = 0;
         for (int u = 0; u < w - s.q; ++u) before += (unsigned)rem_active(s, L, u);
         pc = PaceSeq{Pm, rbase + before * (unsigned)Pm, (unsigned)rem_active(s, L, w - s.q)};
+#ifndef DEIG_AB_SYRK_NO_REM_CHIP
+        if (!s.xm) {  // global item numbering: round u runs min(G, items - u G) items
+          const int items = s.R * s.nseg;
+          unsigned gb = (unsigned)s.q * (P / kChipPaceEvery) * (unsigned)s.G;
+          for (int u = 0; u < w - s.q; ++u)
+            gb += (unsigned)min(s.G, items - u * s.G) * (unsigned)(Pm / kChipPaceEvery);
+          pc.g = true;
+          pc.gbase = gb;
+          pc.gmult = (unsigned)min(s.G, items - (w - s.q) * s.G);
+        }
+#endif
       }
     }
     segment_h<PRIO>(s, lds, tile, k0, k1, slot, partial, pc);
@@ -1069,7 +1106,7 @@ Layout make_layout(int64_t n, int64_t d, int G, int64_t chunk_rows) {
   L.off_order = off;
   off = align_up(off + sizeof(int) * L.T, 256);
   L.off_pace = off;
-  off += 8 * 128;  // 8 XCD counters, one per 128-B line
+  off += 16 * 128;  // 8 XCD counters and the chip-wide one, one per 128-B line
   L.off_accs = off;
   off += sizeof(float) * (size_t)G * SLAB;
   L.off_part = off;
@@ -1259,7 +1296,7 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
     s.beta = accumulate ? 1 : 0;
     s.flush_kt = (int)(flush_rows / ROWS_PAD);
     if (s.flush_kt < 1) s.flush_kt = 1;
-    if (s.pace_kt > 0) DEIG_HIP_CHECK(hipMemsetAsync(s.pace, 0, 8 * 128, stream));
+    if (s.pace_kt > 0) DEIG_HIP_CHECK(hipMemsetAsync(s.pace, 0, 9 * 128, stream));
     hipLaunchKernelGGL((syrks_kernel<16, 2, 2, true>), dim3(G), dim3(NTHR), 0, stream, s);
     DEIG_HIP_CHECK(hipGetLastError());
     if (s.R > 0) {
@@ -1287,7 +1324,7 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
     s.beta = (c > 0 || accumulate) ? 1 : 0;
     s.flush_kt = (int)(flush_rows / (16 * kt_steps));
     const bool mf16 = variant >= 100;  // 162, 163, 1PQR0, 2000R: 16x16x32 slabs
-    if (s.pace_kt > 0) DEIG_HIP_CHECK(hipMemsetAsync(s.pace, 0, 8 * 128, stream));
+    if (s.pace_kt > 0) DEIG_HIP_CHECK(hipMemsetAsync(s.pace, 0, 9 * 128, stream));
     if (variant != 163) launch_split_pass_kernel<kSyrkLarge == 163 ? 162 : kSyrkLarge>(G, stream, s);
     DEIG_HIP_CHECK(hipGetLastError());
     if (s.R > 0) {
