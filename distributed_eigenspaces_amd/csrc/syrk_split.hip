@@ -1053,6 +1053,43 @@ int remainder_segments(int64_t R, int G) {
   return 1;
 }
 
+// Compact XCD groups (r05; G = 256 blocks, nt % 8 == 0): the triangle of nt / 8 = m
+// block rows of 8 tile rows is cut into m diagonal triangles (36 tiles: a group of 32
+// on 8 panels plus 4 left over) and m (m - 1) / 2 off-diagonal 8 x 8 squares (two
+// groups of 8 x 4 tiles on 12 panels each).  Group g holds order[32 g .. 32 g + 31]; in
+// full phase w XCD x runs group 8 w + x (its G / 8 = 32 blocks, one tile each), so an
+// XCD's concurrent tiles share 8-12 panels (the 8 x 4 super-tile order averaged 14.5
+// at config 3: its 32-tile runs straddle super-tiles); the two halves of a square run in
+// the same phase on neighbouring XCDs.  The 4 m leftover tiles end the order: they are
+// the split-K remainder (T mod 256 = 4 m whenever m % 4 == 0).  Groups are listed by
+// block row a: the triangle, then squares (a, 0 .. a - 1); block row a starts at group
+// a^2.  One thread per group.
+__global__ __launch_bounds__(256) void tile_order_compact_kernel(int nt, int* order) {
+  const int m = nt / 8;
+  const int u = blockIdx.x * 256 + threadIdx.x;
+  if (u >= m * m) return;
+  int a = (int)sqrtf((float)u);
+  while (a * a > u) --a;
+  while ((a + 1) * (a + 1) <= u) ++a;
+  const int item = u - a * a;
+  int* grp = order + 32 * u;
+  if (item == 0) {
+    int i = 0;
+    for (int ti = 8 * a; ti < 8 * a + 8; ++ti)
+      for (int tj = 8 * a; tj <= ti; ++tj) {
+        const int v = ti | (tj << 16);
+        if (i < 32) grp[i] = v;
+        else order[32 * m * m + 4 * a + (i - 32)] = v;
+        ++i;
+      }
+  } else {
+    const int b = (item - 1) >> 1, h = (item - 1) & 1;
+    int i = 0;
+    for (int ti = 8 * a; ti < 8 * a + 8; ++ti)
+      for (int tj = 8 * b + 4 * h; tj < 8 * b + 4 * h + 4; ++tj) grp[i++] = ti | (tj << 16);
+  }
+}
+
 // Remainder schedule of the half-ring kernel: bit 0 paces remainder rounds, bit 1
 // numbers remainder items XCD-major.  Default 1 since r04 (interleaved A/B in one
 // process, profiles/r04za_syrk_*_ab.log, unpaced / paced / XCD-major / both): config 2
@@ -1275,9 +1312,15 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
 #endif
   s.xm = (int)L.xm;
   s.rpace = kSyrkRem & 1;
-  hipLaunchKernelGGL(tile_order_kernel,
-                     dim3((unsigned)cdiv(cdiv(s.nt, SUPER_H) * cdiv(s.nt, SUPER_W), 256)), dim3(256), 0, stream, s.nt,
-                     reinterpret_cast<int*>(base + L.off_order));
+#ifndef DEIG_AB_SYRK_SUPER_ORDER
+  if (G == 256 && s.nt % 8 == 0)
+    hipLaunchKernelGGL(tile_order_compact_kernel, dim3((unsigned)cdiv((s.nt / 8) * (s.nt / 8), 256)), dim3(256), 0,
+                       stream, s.nt, reinterpret_cast<int*>(base + L.off_order));
+  else
+#endif
+    hipLaunchKernelGGL(tile_order_kernel,
+                       dim3((unsigned)cdiv(cdiv(s.nt, SUPER_H) * cdiv(s.nt, SUPER_W), 256)), dim3(256), 0, stream,
+                       s.nt, reinterpret_cast<int*>(base + L.off_order));
   DEIG_HIP_CHECK(hipGetLastError());
   s.X = X;
   s.ldx = ldx;
