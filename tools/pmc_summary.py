@@ -26,4 +26,5 @@ if "SQ_VALU_MFMA_BUSY_CYCLES" in c and "GRBM_GUI_ACTIVE" in c:
           f"{c['SQ_VALU_MFMA_BUSY_CYCLES'] / 1024 / (c['GRBM_GUI_ACTIVE'] / 8):.3f}")
 if "SQ_WAVE_CYCLES" in c:
     for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
-        print(f"{k} / WAVE_CYCLES {c[k] / c['SQ_WAVE_CYCLES']:.3f}")
+        if k in c:
+            print(f"{k} / WAVE_CYCLES {c[k] / c['SQ_WAVE_CYCLES']:.3f}")
