@@ -553,6 +553,14 @@ __global__ __launch_bounds__(512) void oja_tn_kernel(const float* __restrict__ X
 // the final copy-out poisons V with NaN - a failure is loud, never a hang.
 constexpr int OB_G = 256, OB_NR = 16, OB_NF = 16, OB_RB = 256, OB_TS = 36;
 constexpr int OB_CNT_LINE = 32;  // one counter per 128-B line
+// Loads in flight in the two 16-partial reductions (steps 2 and 4): all 16 issued
+// before the fixed-order sum (r05; 4 before) - one L2 / fabric round trip per lane
+// instead of four, same sums bit for bit.
+#ifdef DEIG_AB_OJA_RED_UNROLL
+constexpr int kOjaRedUnroll = DEIG_AB_OJA_RED_UNROLL;
+#else
+constexpr int kOjaRedUnroll = 16;
+#endif
 
 struct OjaBlk {
   const float* X;  // first batch of the run
@@ -711,7 +719,7 @@ __global__ __launch_bounds__(512) void oja_blk_kernel(OjaBlk a) {
       const int rql = t / KP, col = t - rql * KP;
       const int64_t rq = (R0 + 16 * j) / 4 + rql;
       f32x4 s = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
+#pragma unroll kOjaRedUnroll
       for (int jj = 0; jj < OB_NF; ++jj)
         s += __builtin_bit_cast(f32x4, ob_ld(rp, (uint32_t)((((int64_t)jj * (b / 4) + rq) * KP + col) * 16)));
 #pragma unroll
@@ -817,8 +825,13 @@ __global__ __launch_bounds__(512) void oja_blk_kernel(OjaBlk a) {
       if (g < FB / 8) {
         f32x4 sm = {0.f, 0.f, 0.f, 0.f};
         const int64_t fq = (F0 + 8 * g) / 4 + q;
+        // this lane's V entries first (independent of the partials: their loads
+        // overlap the partials' instead of following the sum)
+        float vo[4] = {0.f, 0.f, 0.f, 0.f};
         if (col < KP) {
-#pragma unroll 4
+#pragma unroll
+          for (int e = 0; e < 4; ++e) vo[e] = a.V[(4 * fq + e) * KP + col];
+#pragma unroll kOjaRedUnroll
           for (int ii = 0; ii < OB_NR; ++ii)
             sm += __builtin_bit_cast(f32x4, ob_ld(rq, (uint32_t)((((int64_t)ii * (d / 4) + fq) * KP + col) * 16)));
         }
@@ -828,7 +841,7 @@ __global__ __launch_bounds__(512) void oja_blk_kernel(OjaBlk a) {
           const int64_t f = 4 * fq + e;
           v[e] = 0.f;
           if (col < KP) {
-            v[e] = fmaf(a.coef, sm[e], a.V[f * KP + col]);
+            v[e] = fmaf(a.coef, sm[e], vo[e]);
             a.V[f * KP + col] = v[e];
           }
         }
