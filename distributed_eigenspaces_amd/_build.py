@@ -18,8 +18,11 @@ SOURCES = ["capi.hip", "syrk.hip", "syrk_split.hip", "syrk_u8.hip", "skinny.hip"
 # Per-source extra flags.  sweep.hip: keep the split's scalar f32 subtractions
 # unpacked (v_pk_add_f32 beside MFMAs costs issue cycles, MI355X_MICROARCH.md).
 EXTRA_FLAGS = {"sweep.hip": ["-fno-slp-vectorize"], "syrk_split.hip": ["-fno-slp-vectorize"]}
-HEADERS = ["deig_internal.hpp", os.path.join("..", "..", "include", "deig.h"),
-           os.path.join("ab", "syrk_split_superseded.inc")]
+HEADERS = ["deig_internal.hpp", os.path.join("..", "..", "include", "deig.h")]
+# Test-only variant (tests/test_gpu_oja_timeout.py): oja.hip with a zero spin bound, so
+# every resident hand-off times out and the DEIG_ETIMEOUT report can be exercised; the
+# other objects are the shipped library's.
+OJA_TIMEOUT_LIB = os.path.join(HERE, "libdeig_test_oja_timeout.so")
 ARCH = os.environ.get("DEIG_OFFLOAD_ARCH", "gfx950")
 
 
@@ -72,6 +75,29 @@ def build_library(force: bool = False, verbose: bool = True, defines=(), out: st
     if verbose:
         sys.stderr.write(f"built {lib}\n")
     return lib
+
+
+def build_oja_timeout_lib(verbose: bool = True) -> str:
+    """The test-only variant OJA_TIMEOUT_LIB (oja.hip with -DDEIG_AB_OJA_SPIN_TICKS=0,
+    linked with the shipped library's other objects; build_library first)."""
+    tmpdir = os.path.join(HERE, "build")
+    hipcc = _hipcc()
+    obj = os.path.join(tmpdir, "oja_timeout.o")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+           "-Wno-inline-asm", "-DDEIG_AB_OJA_SPIN_TICKS=0", "-c", os.path.join(CSRC, "oja.hip"), "-o", obj]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    if r.returncode != 0:
+        raise RuntimeError("hipcc failed:\n" + " ".join(cmd) + "\n" + r.stdout.decode())
+    objs = [obj if s == "oja.hip" else os.path.join(tmpdir, s.replace(".hip", ".o")) for s in SOURCES]
+    tmp_lib = OJA_TIMEOUT_LIB + ".tmp"
+    r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp_lib] + objs,
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    if r.returncode != 0:
+        raise RuntimeError("link failed:\n" + r.stdout.decode())
+    os.replace(tmp_lib, OJA_TIMEOUT_LIB)
+    if verbose:
+        sys.stderr.write(f"built {OJA_TIMEOUT_LIB}\n")
+    return OJA_TIMEOUT_LIB
 
 
 if __name__ == "__main__":

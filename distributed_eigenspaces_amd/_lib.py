@@ -6,6 +6,7 @@ There is no CPU fallback: if the library is missing the import of an op raises.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import re
@@ -22,6 +23,7 @@ DEIG_NOT_CONVERGED = 1
 DEIG_EINVAL = -1
 DEIG_EHIP = -2
 DEIG_EWORKSPACE = -3
+DEIG_ETIMEOUT = -4
 DEIG_SYRK_AUTO = 0
 DEIG_SYRK_SPLIT3 = 1
 DEIG_SYRK_FP32 = 2
@@ -71,6 +73,8 @@ _fp = ctypes.c_void_p  # device pointers are passed as integers
 
 SIGNATURES = {
     "deig_version": (ctypes.c_int, []),
+    "deig_shutdown": (None, []),
+    "deig_oja_error": (ctypes.c_int, [_vp, _c_sz, _c_i64, _c_i64, ctypes.c_int, _vp]),
     "deig_last_error": (ctypes.c_char_p, []),
     "deig_syrk_f32": (ctypes.c_int, [_fp, _c_i64, _c_i64, _c_i64, ctypes.c_float, _fp, _c_i64,
                                      _vp, _c_sz, _vp]),
@@ -160,6 +164,11 @@ class DeigError(RuntimeError):
     """A libdeig call failed (HIP error or workspace problem)."""
 
 
+class DeigTimeoutError(DeigError):
+    """A resident Oja run's hand-off waited past its bound (DEIG_ETIMEOUT): the basis
+    it wrote is NaN (CUs held by other work kept its grid from being co-resident)."""
+
+
 class NotConvergedWarning(RuntimeWarning):
     """The eigensolver stopped at max_sweeps above its residual tolerance."""
 
@@ -187,7 +196,19 @@ def lib() -> ctypes.CDLL:
                 fn.restype = res
                 fn.argtypes = args
             _lib = L
+            # free the library's pinned host blocks while the HIP runtime is alive:
+            # Python's atexit runs before the C runtime's exit handlers (and the HIP
+            # runtime's teardown), include/deig.h deig_shutdown
+            atexit.register(_shutdown)
     return _lib
+
+
+def _shutdown():
+    if _lib is not None:
+        try:
+            _lib.deig_shutdown()
+        except Exception:  # noqa: BLE001 - never raise from an exit handler
+            pass
 
 
 def solver_opts(**fields) -> SolverOpts:
@@ -215,4 +236,6 @@ def check(rc: int, what: str) -> int:
     msg = f"{what}: {last_error()} (code {rc})"
     if rc == DEIG_EINVAL:
         raise ValueError(msg)
+    if rc == DEIG_ETIMEOUT:
+        raise DeigTimeoutError(msg)
     raise DeigError(msg)

@@ -78,6 +78,13 @@ constexpr int kMaxDeflate = 8;
 // scale, kNegTarget * theta_target) restarts the solve on S + sigma I,
 // sigma = kShiftGrow * |theta_min| (at most kMaxShifts restarts).
 constexpr float kNegRel = 1e-5f;
+// Deflation-residue band of the convergence test (cycle_finish): a block whose largest
+// |Ritz value| is at most kBandRel * |lambda_max| is judged by its residual against
+// |lambda_max| (its own ~0 Ritz values never reach tol).  32 fp32 ulps of the scale:
+// the level of deflation residue and fp32 rounding of S, not of small but genuine
+// eigenvalues (the band at kNegRel = 1e-5 also took eigenvalues up to 1e-5
+// of lambda_max, whose own-relative residual then only reached ~0.1).
+constexpr float kBandRel = 32.f * 1.1920929e-7f;
 constexpr float kNegTarget = 0.1f;
 constexpr double kShiftGrow = 1.1;
 constexpr int kMaxShifts = 2;
@@ -375,6 +382,14 @@ class StatusPool {
     std::lock_guard<std::mutex> lk(mu_);
     free_.push_back(p);
   }
+  // deig_shutdown: free the idle blocks while the HIP runtime is alive (blocks in use by
+  // a running solver come back through release and stay until the next drain)
+  void drain() {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (HostStatus* p : free_) (void)hipHostFree(p);
+    free_.clear();
+    (void)hipGetLastError();
+  }
 
  private:
   std::mutex mu_;
@@ -601,7 +616,7 @@ struct Solver {
     band_f = 1.f;
     if (abs_scale > 0.f) {
       const float blk = fmaxf(fabsf(lam_h[0]), 1e-30f);
-      if (blk <= kNegRel * abs_scale) band_f = blk / abs_scale;
+      if (blk <= kBandRel * abs_scale) band_f = blk / abs_scale;
     }
     last = res_h[kc] * band_f;
     // Ritz pairs of a capped Jacobi that stopped short are approximate: their
@@ -1306,7 +1321,13 @@ using namespace deig;
 
 extern "C" {
 
-int deig_version(void) { return 0x000500; }
+int deig_version(void) { return 0x000600; }
+
+void deig_shutdown(void) {
+  (void)hipDeviceSynchronize();
+  status_pool().drain();
+  (void)hipGetLastError();
+}
 
 const char* deig_last_error(void) { return g_err; }
 
@@ -1609,6 +1630,11 @@ int deig_oja_steps_ex(const float* X, int64_t nb, int64_t b, int64_t d, int64_t 
   if (!X || !V || !aligned16(X)) return fail(DEIG_EINVAL, "oja: X must be 16-byte aligned");
   return oja_steps_launch(X, nb, b, d, ldx, eta, V, k, ldv, orth_every, ws, ws_bytes,
                           (hipStream_t)stream, algo);
+}
+
+int deig_oja_error(const void* ws, size_t ws_bytes, int64_t b, int64_t d, int k, void* stream) {
+  g_err[0] = 0;
+  return oja_error(ws, ws_bytes, b, d, k, (hipStream_t)stream);
 }
 
 int deig_oja_steps_f32(const float* X, int64_t nb, int64_t b, int64_t d, int64_t ldx, float eta,

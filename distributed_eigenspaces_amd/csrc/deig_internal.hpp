@@ -223,6 +223,7 @@ int oja_launch(const float* Xb, int64_t b, int64_t d, int64_t ldx, float eta, fl
 int oja_steps_launch(const float* X, int64_t nb, int64_t b, int64_t d, int64_t ldx, float eta,
                      float* V, int k, int64_t ldv, int orth_every, void* ws, size_t ws_bytes,
                      hipStream_t stream, int algo);
+int oja_error(const void* ws, size_t ws_bytes, int64_t b, int64_t d, int k, hipStream_t st);
 
 // Projection Y = X W (project.hip).
 size_t project_workspace_bytes(int64_t n, int64_t d, int k);

@@ -599,12 +599,20 @@ __device__ __forceinline__ u32x4 ob_ld(const __amdgpu_buffer_rsrc_t& r, uint32_t
 __device__ __forceinline__ void ob_signal(unsigned* c) {
   __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Spin bound of one hand-off wait in wall_clock64 ticks (100 MHz): 2 s.  Test builds
+// only (-DDEIG_AB_OJA_SPIN_TICKS=0, tests/test_gpu_oja_timeout.py) shrink it so that
+// waits time out and the timeout report (deig_oja_error) can be exercised.
+#ifdef DEIG_AB_OJA_SPIN_TICKS
+constexpr uint64_t kOjaSpinTicks = DEIG_AB_OJA_SPIN_TICKS;
+#else
+constexpr uint64_t kOjaSpinTicks = 200000000ull;
+#endif
 // One lane: wait until *c >= target (bounded; see above).
 __device__ __forceinline__ void ob_wait(unsigned* c, unsigned target, unsigned* err) {
   const uint64_t t0 = wall_clock64();
   while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
     if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-    if (wall_clock64() - t0 > 200000000ull) {
+    if (wall_clock64() - t0 >= kOjaSpinTicks) {
       __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
@@ -1157,6 +1165,24 @@ int oja_steps_launch(const float* X, int64_t nb, int64_t b, int64_t d, int64_t l
   hipLaunchKernelGGL(rowpad_to_col, dim3((unsigned)cdiv(d * k, 256)), dim3(256), 0, st, cur, d, k,
                      kp, V, ldv, o.err);
   DEIG_HIP_CHECK(hipGetLastError());
+  return DEIG_OK;
+}
+
+// The timeout word of the last oja_steps_launch on this workspace (set by a resident
+// hand-off that waited past its bound; V was then written as NaN).  Synchronises st.
+int oja_error(const void* ws, size_t ws_bytes, int64_t b, int64_t d, int k, hipStream_t st) {
+  DEIG_REQUIRE(k >= 1 && k <= 64 && b >= 1 && d >= 4, "oja_error: bad shape");
+  const int kp = (int)cdiv(k, 16) * 16;
+  size_t total = 0;
+  OjaWs o = carve_oja(const_cast<void*>(ws), ws_bytes, b, d, kp, &total);
+  if (!ws || total > ws_bytes)
+    return fail(DEIG_EWORKSPACE, "oja_error: workspace %zu < %zu", ws_bytes, total);
+  unsigned e = 0;
+  DEIG_HIP_CHECK(hipMemcpyAsync(&e, o.err, sizeof(e), hipMemcpyDeviceToHost, st));
+  DEIG_HIP_CHECK(hipStreamSynchronize(st));
+  if (e)
+    return fail(DEIG_ETIMEOUT, "oja: a resident hand-off waited past its bound (CUs held by other "
+                               "work?); V was written as NaN");
   return DEIG_OK;
 }
 

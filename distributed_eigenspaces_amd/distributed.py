@@ -31,11 +31,8 @@ reference accepts):
 from __future__ import annotations
 
 import argparse
-import hashlib
 import json
-import threading
 import time
-import weakref
 from contextlib import nullcontext
 
 import numpy as np
@@ -54,77 +51,32 @@ def _is_numpy(x) -> bool:
     return isinstance(x, np.ndarray) or not isinstance(x, torch.Tensor)
 
 
-_dev_cache: dict = {}
-_dev_lock = threading.Lock()
-
-
-def _fingerprint(a: np.ndarray):
-    """Cheap content check of a host array: shape, dtype and a hash of up to 64K
-    evenly spaced elements (catches ``data[:] = new`` on a reused buffer)."""
-    flat = a.reshape(-1)
-    step = max(1, flat.size // 65536)
-    return (a.shape, a.dtype.str, hashlib.blake2b(np.ascontiguousarray(flat[::step]).tobytes(),
-                                                  digest_size=16).digest())
-
-
-def _drop(key):
-    with _dev_lock:
-        _dev_cache.pop(key, None)
-
-
-def clear_device_cache():
-    """Forget every cached device copy of node data (see ``_device_copy``)."""
-    with _dev_lock:
-        _dev_cache.clear()
-
-
-def _device_copy(data) -> torch.Tensor:
-    """The node's data on the GPU, shared by every node given the same host array
-    (threaded workers hold one device copy).  uint8 samples stay uint8 (the exact
-    integer covariance path), float64 stays float64 (the reference's dtype: the
-    mean-shifted covariance path), everything else becomes float32.
-
-    The cache holds the device copy only while the host array is alive (weak
-    reference; the entry is dropped when the array is freed) and re-uploads when a
-    sampled fingerprint of the array's contents changed.  ``clear_device_cache()``
-    forgets everything."""
-    if isinstance(data, torch.Tensor) and data.is_cuda and \
-            data.dtype in (torch.uint8, torch.float32, torch.float64):
-        return data
+def _rows_to_device(data, lo: int, hi: int) -> torch.Tensor:
+    """Rows [lo, hi) of the node's data on the GPU, read from ``data`` on every call
+    like the reference's ``self.data[lo:hi]`` (distributed.py:46).  A GPU tensor is
+    sliced in place (no copy); host data (numpy, CPU tensors, array-likes) has only
+    the requested rows uploaded, so a write to the host array between requests is
+    always seen - there is no device-side cache to go stale.  uint8 samples stay
+    uint8 (the exact integer covariance path), float64 stays float64 (the
+    reference's dtype: the mean-shifted covariance path), everything else becomes
+    float32.  To keep one resident copy for many requests, hand the node a GPU
+    tensor."""
+    if isinstance(data, torch.Tensor) and data.is_cuda:
+        rows = data[lo:hi]
+        if rows.dtype in (torch.uint8, torch.float32, torch.float64):
+            return rows
+        return linalg.require_device_tensor(rows, "SlaveNode.data")
     if not torch.cuda.is_available():
         raise RuntimeError("SlaveNode: needs a ROCm GPU; there is no CPU fallback")
-    if isinstance(data, np.ndarray):
-        # always sampled: a read-only flag can be switched back on, written and locked
-        fp = _fingerprint(data)
-    elif isinstance(data, torch.Tensor):
-        # a CPU tensor: storage, in-place version counter AND the sampled contents
-        # (writes through an aliasing numpy array or raw pointers bypass _version)
-        try:
-            content = _fingerprint(data.detach().numpy())
-        except (TypeError, RuntimeError):  # a dtype numpy cannot view: never cached
-            content = None
-        fp = None if content is None else (data.data_ptr(), data._version, content)
+    if isinstance(data, torch.Tensor):
+        rows = data[lo:hi]
     else:
-        fp = None  # other array-likes: converted on every call, never cached
-    key = id(data)
-    if fp is not None:
-        with _dev_lock:
-            hit = _dev_cache.get(key)
-            if hit is not None and hit[0]() is data and hit[1] == fp:
-                return hit[2]
-    t = torch.as_tensor(data)
-    if t.dtype == torch.uint8:
-        dev = t.to(torch.device("cuda", torch.cuda.current_device()))
-    else:
-        dev = linalg.require_device_tensor(t, "SlaveNode.data", keep_f64=True)
-    if fp is not None:
-        try:
-            ref = weakref.ref(data, lambda _r, k=key: _drop(k))
-        except TypeError:  # not weak-referenceable: no caching
-            return dev
-        with _dev_lock:
-            _dev_cache[key] = (ref, fp, dev)
-    return dev
+        a = np.asarray(data[lo:hi])
+        # torch cannot wrap a read-only array without a warning: copy those rows
+        rows = torch.from_numpy(a if a.flags.writeable else a.copy())
+    if rows.dtype == torch.uint8:
+        return rows.to(torch.device("cuda", torch.cuda.current_device()))
+    return linalg.require_device_tensor(rows, "SlaveNode.data", keep_f64=True)
 
 
 def top_k_eigh(matrix, k: int):
@@ -174,34 +126,34 @@ class Node:
 
 
 class SlaveNode(Node):
-    """distributed.py:32-70: worker.  Keeps a device copy of ``data`` so each
-    request only slices it (the reference slices a host view, :46)."""
+    """distributed.py:32-70: worker.  Each request reads rows [lo, hi) of ``data``
+    (distributed.py:46): a GPU tensor is sliced in place, host data has those rows
+    uploaded (``_rows_to_device``)."""
 
     def __init__(self, broker_host, data):
         super().__init__(broker_host)
         print("Slave Start listening")
         self.data = data
-        self._dev = None
         self._stream = None
         self.channel.basic_consume(queue="slaves", on_message_callback=self.callback_)
 
     def start(self):
         self.channel.start_consuming()
 
-    def _device_data(self):
-        if self._dev is None:
-            self._dev = _device_copy(self.data)
-        return self._dev
+    def _device_rows(self, lo, hi):
+        return _rows_to_device(self.data, lo, hi)
 
     def callback_(self, channel, method, properties, body):
         request = json.loads(body)
         print("Slave: Received, batchid: " + str(request["batch"]))
         lo, hi = request["batch"][0], request["batch"][1]
-        data = self._device_data()
-        if self._stream is None and data.is_cuda:  # one HIP stream per node: threaded nodes overlap
-            self._stream = torch.cuda.Stream(data.device)
+        batch = self._device_rows(lo, hi)
+        if batch.is_cuda:
+            if self._stream is None:  # one HIP stream per node: threaded nodes overlap
+                self._stream = torch.cuda.Stream(batch.device)
+            # the rows were uploaded (or written) on the current stream
+            self._stream.wait_stream(torch.cuda.current_stream(batch.device))
         with (torch.cuda.stream(self._stream) if self._stream is not None else nullcontext()):
-            batch = data[lo:hi]
             eigenspace = self.compute_sigma_hat_(batch)
             eigenspace = self.top_k_eigenvectors(eigenspace, request["rank"])
             response = dict()

@@ -23,7 +23,7 @@ from . import _lib
 __all__ = [
     "sigma_hat", "topk_eigh", "topk_eigh_batch", "projavg_topk", "oja_step", "default_subspace",
     "EigResult", "require_device_tensor", "project", "stack_bases", "gemm_skinny",
-    "oja_steps", "sym_apply", "sym_power", "sigma_hat_u8", "sigma_hat_shift",
+    "oja_steps", "oja_check", "sym_apply", "sym_power", "sigma_hat_u8", "sigma_hat_shift",
 ]
 
 DEFAULT_TOL = 1e-6
@@ -524,11 +524,24 @@ def oja_step(Xb: torch.Tensor, V: torch.Tensor, eta: float) -> torch.Tensor:
                                  V.data_ptr(), k, V.stride(1), ws.data_ptr(), nbytes,
                                  _stream(Xb.device))
     _lib.check(rc, "deig_oja_step_f32")
+    oja_check(Xb.device, b, d, k)
     return V
 
 
+def oja_check(device, b: int, d: int, k: int) -> None:
+    """Raise ``DeigTimeoutError`` if the last Oja call on this thread's workspace for
+    (b, d, k) on ``device`` timed out in a resident hand-off (its basis is NaN);
+    synchronises that device's current stream (include/deig.h deig_oja_error)."""
+    L = _lib.lib()
+    with torch.cuda.device(device):
+        nbytes = L.deig_oja_workspace(b, d, k)
+        ws = _workspace(device, nbytes)
+        rc = L.deig_oja_error(ws.data_ptr(), nbytes, b, d, k, _stream(device))
+    _lib.check(rc, "oja")
+
+
 def oja_steps(X: torch.Tensor, V: torch.Tensor, eta: float, batch: int,
-              orth_every: int = 8, algo: str = "auto") -> torch.Tensor:
+              orth_every: int = 8, algo: str = "auto", check: bool = True) -> torch.Tensor:
     """In-place Oja over the consecutive row batches X[i*batch:(i+1)*batch] (config 4).
 
     One C call for all batches (no host work in between); the basis is
@@ -536,7 +549,11 @@ def oja_steps(X: torch.Tensor, V: torch.Tensor, eta: float, batch: int,
     span of per-batch orthonormalisation (``oja_step`` in a loop) because the update
     is linear in V.  Rows beyond the last full batch are ignored.  ``algo``
     (include/deig.h DEIG_OJA_*): "auto", "two_pass" or "resident" (Xb read once per
-    batch; batch = 4096, d a multiple of 512 up to 3072, k <= 32).  Returns V."""
+    batch; batch = 4096, d a multiple of 512 up to 3072, k <= 32).  ``check`` (default):
+    synchronise and raise ``DeigTimeoutError`` if a resident hand-off timed out (V is
+    then NaN); ``check=False`` leaves the call asynchronous - then call ``oja_check``
+    before any other op on this thread's stream (they share the workspace that holds
+    the timeout word).  Returns V."""
     X = _rowmajor_4(require_device_tensor(X, "oja_steps"), "X")
     n, d = X.shape
     b = int(batch)
@@ -555,6 +572,8 @@ def oja_steps(X: torch.Tensor, V: torch.Tensor, eta: float, batch: int,
                                  V.data_ptr(), k, V.stride(1), int(orth_every),
                                  _lib.OJA_ALGOS[algo], ws.data_ptr(), nbytes, _stream(X.device))
     _lib.check(rc, "deig_oja_steps_ex")
+    if check:
+        oja_check(X.device, b, d, k)
     return V
 
 

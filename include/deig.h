@@ -37,13 +37,23 @@ extern "C" {
 #define DEIG_EINVAL (-1)
 #define DEIG_EHIP (-2)
 #define DEIG_EWORKSPACE (-3)
+#define DEIG_ETIMEOUT (-4) /* a resident Oja hand-off timed out (deig_oja_error) */
 
 /* Element types of float inputs (deig_syrk_shift, deig_topk_sym_ex). */
 #define DEIG_F32 0
 #define DEIG_F64 1
 
-/* Library version, e.g. 0x000400 for 0.4.0. */
+/* Library version, e.g. 0x000400 for 0.4.0.  A caller built against an older header
+ * should compare it with the version it was built for before binding entry points
+ * whose signature changed (deig_topk_sym_batch: see below). */
 int deig_version(void);
+
+/* Release the library's process-lifetime host resources (the pinned per-cycle status
+ * blocks of the eigensolvers) after synchronising the current device.  Optional; call
+ * it at process exit BEFORE the HIP runtime is torn down (the Python binding registers
+ * it with atexit, which runs before the C runtime's exit handlers).  No solver may be
+ * running; later solver calls allocate new blocks. */
+void deig_shutdown(void);
 
 /* Thread-local message for the last nonzero return on this thread ("" if none). */
 const char* deig_last_error(void);
@@ -280,7 +290,9 @@ int deig_topk_sym_batch_ex(int W, const void* const* S, int stype, int64_t d, in
 /* The r03 (0x000300) signature, unchanged: deig_topk_sym_batch_ex with
  * status_out = NULL.  streams: ignored since 0x000400 (r03 ran one stream per
  * problem; may be NULL).  (0x000400 had inserted status_out into THIS signature, an
- * in-place ABI break; 0x000500 restores it and moves status_out to the _ex form.) */
+ * in-place ABI break; 0x000500 restores it and moves status_out to the _ex form.  A
+ * binary built against the 0x000400 header links but passes status_out where opts is
+ * read: check deig_version() >= 0x000500 before calling, or call the _ex form.) */
 int deig_topk_sym_batch(int W, const void* const* S, int stype, int64_t d, int64_t lds, int k, int p,
                         int max_sweeps, float tol, float* const* V, int64_t ldv, float* const* evals,
                         int* sweeps_out, float* resid_out, const deig_solver_opts* opts, void* ws,
@@ -324,14 +336,21 @@ int deig_oja_steps_f32(const float* X, int64_t nb, int64_t b, int64_t d, int64_t
  * >= 256 CUs) before its plain launch: when it does not fit, DEIG_OJA_RESIDENT
  * returns DEIG_EHIP and DEIG_OJA_AUTO runs the two-pass path.  If a hand-off still
  * waits longer than 2 s (CUs held by other persistent work), V comes back all NaN -
- * the call is asynchronous, so NaN in V is how such a timeout is reported.  Same
- * workspace as deig_oja_steps_f32. */
+ * the call is asynchronous, so NaN in V is how such a timeout shows in the data, and
+ * deig_oja_error reports it as an error.  Same workspace as deig_oja_steps_f32. */
 #define DEIG_OJA_AUTO 0
 #define DEIG_OJA_TWO_PASS 1
 #define DEIG_OJA_RESIDENT 2
 int deig_oja_steps_ex(const float* X, int64_t nb, int64_t b, int64_t d, int64_t ldx, float eta,
                       float* V, int k, int64_t ldv, int orth_every, int algo, void* ws,
                       size_t ws_bytes, void* stream);
+
+/* Status of the last deig_oja_steps_ex / deig_oja_steps_f32 / deig_oja_step_f32 call
+ * on workspace ws (same b, d, k): synchronises `stream`, then returns DEIG_ETIMEOUT if
+ * a resident hand-off of that call waited past its 2-s bound (V was written as NaN),
+ * else DEIG_OK.  Call it before the next Oja call on the same workspace (each call
+ * clears the word). */
+int deig_oja_error(const void* ws, size_t ws_bytes, int64_t b, int64_t d, int k, void* stream);
 
 /* Projection onto an estimated eigenspace: Y = X W.
  * Replaces the notebook's  online_distributed_PCA = lambda X: X @ matrix_w

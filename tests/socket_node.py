@@ -19,8 +19,8 @@ from distributed_eigenspaces_amd import distributed as dd  # noqa: E402
 
 
 class OracleSlave(dd.SlaveNode):
-    def _device_data(self):
-        return torch.from_numpy(np.asarray(self.data, dtype=np.float64))
+    def _device_rows(self, lo, hi):
+        return torch.from_numpy(np.asarray(self.data[lo:hi], dtype=np.float64))
 
     def compute_sigma_hat_(self, x):
         from oracle import ref_cpu

@@ -35,7 +35,7 @@ def test_header_constants_match_bindings():
 
 def test_version_and_error_string():
     L = _lib.lib()
-    assert L.deig_version() == 0x000500
+    assert L.deig_version() == 0x000600
     assert isinstance(_lib.last_error(), str)
 
 

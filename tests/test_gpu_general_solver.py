@@ -205,3 +205,24 @@ def test_k_above_128_rank_deficient(cuda):
         assert np.abs(ev[:k - rank]).max() <= 1e-5 * lmax
         R = S_h @ V - V * ev
         assert np.linalg.norm(R, axis=0).max() <= 1e-4 * lmax
+
+
+def test_k_above_128_small_genuine_eigenvalues(cuda):
+    """k = 300 > 128 whose third block holds only small but genuine eigenvalues,
+    5e-6 .. 9e-6 of lambda_max (the deflation-residue band used to take
+    every block whose Ritz values were <= 1e-5 |lambda_max| and accept it at a residual
+    of ~0.1 relative to its own eigenvalues).  They sit above the band now (32 fp32
+    ulps of the scale), so they converge to their own relative tolerance: eigenvalues
+    within the north_star 1e-5 and the subspace of the whole top-k at the bar."""
+    import distributed_eigenspaces_amd as de
+    d, k = 512, 300
+    lam = np.concatenate([np.linspace(10.0, 1.0, 224), np.linspace(9e-5, 5e-5, 76),
+                          np.linspace(1e-5, 0.0, d - 300)])
+    S, S_h = planted(d, lam, seed=13, device=cuda)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        r = de.topk_eigh(S, k)
+    w, Vr = ref_cpu.top_k_eigh(S_h, k)
+    ev = r.evals.double().cpu().numpy()
+    np.testing.assert_allclose(ev, w, rtol=EV_TOL)
+    assert ref_cpu.projector_distance(r.V.double().cpu().numpy()[:, -224:], Vr[:, -224:]) <= P_TOL

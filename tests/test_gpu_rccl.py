@@ -6,10 +6,13 @@ N > 1 - and the very calls the product makes: ``estimator.gather_bases`` (ONE
 ``streaming.broadcast_basis`` (ONE ``broadcast``).  The exchange replaces the
 reference's AMQP round trip of the bases (reference/distributed.py:55-57, 117-139).
 
-A one-GPU box can only host ranks that share cuda:0; RCCL refuses two ranks on one
-device, so the multi-rank case is tried and skipped with RCCL's reason when it does,
-and the world-1 group still drives RCCL's communicator and kernels through the
-product's functions (with the world-size shortcut bypassed for the test)."""
+Rank r runs on cuda:r whenever the box has at least `world` GPUs (the layout
+``bench.py --gpus N`` uses: LOCAL_RANK -> cuda:LOCAL_RANK), so the multi-rank tests
+run as they are on a multi-GPU box.  A one-GPU box can only host ranks that share
+cuda:0; RCCL refuses two ranks on one device, so there the multi-rank exchange is tried
+and skipped with RCCL's reason, the estimator test skips, and the world-1 group still
+drives RCCL's communicator and kernels through the product's functions (with the
+world-size shortcut bypassed for the test)."""
 import os
 import socket
 
@@ -29,13 +32,18 @@ def _free_port():
     return p
 
 
+def _rank_device(rank, world):
+    """cuda:rank when every rank has a GPU of its own, else all ranks on cuda:0."""
+    return torch.device("cuda", rank if torch.cuda.device_count() >= world else 0)
+
+
 def _rank(rank, world, port, outdir):
     import torch.distributed as dist
 
     from distributed_eigenspaces_amd import estimator, streaming
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                       HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
-    dev = torch.device("cuda", 0)
+    dev = _rank_device(rank, world)
     torch.cuda.set_device(dev)
     try:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
@@ -74,10 +82,11 @@ def _expected(world):
     return torch.cat(parts).numpy(), parts[0].numpy()
 
 
-def _run(world, tmp_path):
+def _run(world, tmp_path, target=None):
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    procs = [ctx.Process(target=target or _rank, args=(r, world, port, str(tmp_path)))
+             for r in range(world)]
     for p in procs:
         p.start()
     hung = False
@@ -103,11 +112,73 @@ def test_rccl_gather_and_broadcast_world1(cuda, tmp_path):
     assert np.array_equal(np.load(tmp_path / "vt0.npy"), V0)
 
 
-def test_rccl_two_ranks_sharing_one_gpu(cuda, tmp_path):
+def test_rccl_two_ranks(cuda, tmp_path):
+    """Two ranks: on cuda:0 and cuda:1 when the box has two GPUs (must pass), else both
+    on cuda:0 (RCCL refuses that: skipped with its reason)."""
     errs = _run(2, tmp_path)
     if errs:
-        pytest.skip(f"RCCL with two ranks on one device: {errs[0][:200]}")
+        if torch.cuda.device_count() >= 2:
+            pytest.fail(f"RCCL on two devices: {errs}")
+        pytest.skip(f"one GPU: RCCL with two ranks on one device: {errs[0][:200]}")
     Wt_exp, V0 = _expected(2)
     for r in range(2):
         assert np.array_equal(np.load(tmp_path / f"wt{r}.npy"), Wt_exp), "all-gather in rank order"
         assert np.array_equal(np.load(tmp_path / f"vt{r}.npy"), V0), "broadcast from rank 0"
+
+
+def _rank_fit(rank, world, port, outdir):
+    """One rank of the product's estimator over RCCL: rank r on cuda:r, one logical
+    worker on its shard of distributed.py:99-104's split, the bases all-gathered
+    (ncclAllGather), the server solve on rank 0."""
+    import torch.distributed as dist
+
+    from distributed_eigenspaces_amd.estimator import DistributedEigenspaceEstimator, rank_shards
+    from tests.conftest import load_golden
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    dev = _rank_device(rank, world)
+    torch.cuda.set_device(dev)
+    try:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        g = load_golden("spiked_d256_k10_m8")
+        X = torch.from_numpy(g["X"].astype(np.float32)).to(dev)
+        (lo, hi), = rank_shards(X.shape[0], world, rank, 1)
+        r = DistributedEigenspaceEstimator(int(g["k"]), workers_per_rank=1).fit(X[lo:hi])
+        torch.cuda.synchronize()
+        np.save(os.path.join(outdir, f"wt{rank}.npy"), r.Wt.cpu().numpy())
+        if r.V is not None:
+            np.save(os.path.join(outdir, f"v{rank}.npy"), r.V.cpu().numpy())
+            np.save(os.path.join(outdir, f"ev{rank}.npy"), r.evals.cpu().numpy())
+        with open(os.path.join(outdir, f"backend{rank}.txt"), "w") as f:
+            f.write(dist.get_backend())
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # reported to the parent
+        with open(os.path.join(outdir, f"error{rank}.txt"), "w") as f:
+            f.write(f"{type(e).__name__}: {e}")
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_rccl_estimator_fit_on_distinct_gpus(cuda, tmp_path, world):
+    """``DistributedEigenspaceEstimator.fit`` with ``world`` ranks on ``world`` GPUs over
+    RCCL == the single-process estimator with ``world`` logical workers on one GPU, bit
+    for bit (the same shards, kernels and gather order: the exchange only moves bytes).
+    Replaces the reference's AMQP exchange of bases (distributed.py:55-57, 117-139).
+    Skips on a box with fewer than ``world`` GPUs (RCCL refuses shared devices)."""
+    if torch.cuda.device_count() < world:
+        pytest.skip(f"needs {world} GPUs, this box has {torch.cuda.device_count()}")
+    from distributed_eigenspaces_amd.estimator import DistributedEigenspaceEstimator
+    from tests.conftest import load_golden
+    g = load_golden("spiked_d256_k10_m8")
+    n = g["X"].shape[0] // world * world
+    X = torch.from_numpy(g["X"][:n].astype(np.float32)).to(cuda)
+    ref = DistributedEigenspaceEstimator(int(g["k"]), workers_per_rank=world).fit(X)
+    errs = _run(world, tmp_path, target=_rank_fit)
+    assert not errs, errs
+    for r in range(world):
+        assert open(tmp_path / f"backend{r}.txt").read() == "nccl"
+        assert np.array_equal(np.load(tmp_path / f"wt{r}.npy"), ref.Wt.cpu().numpy()), \
+            f"rank {r}: gathered bases differ from the one-GPU stack"
+    assert np.array_equal(np.load(tmp_path / "v0.npy"), ref.V.cpu().numpy())
+    assert np.array_equal(np.load(tmp_path / "ev0.npy"), ref.evals.cpu().numpy())
+    assert not (tmp_path / "v1.npy").exists(), "only the server rank solves"

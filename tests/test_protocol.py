@@ -17,8 +17,8 @@ from tests.conftest import load_golden
 
 
 class FakeSlave(dd.SlaveNode):
-    def _device_data(self):
-        return torch.as_tensor(self.data)
+    def _device_rows(self, lo, hi):
+        return torch.as_tensor(self.data[lo:hi])
 
     def compute_sigma_hat_(self, x):
         return x  # pass the rows through; the fake basis encodes the shard
