@@ -1288,7 +1288,7 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
   // smallest at flush_rows ~ sqrt(32 n); each flush is a read-add-write of the block's
   // 256 KiB slab beside stalled MFMAs, and the measured error grows slowly above that
   // point, so the rule is 2^floor(log2 sqrt(128 n)) within [4096, 16384] (r05,
-  // interleaved A/B with a float64 check of 64 sampled columns, tools/syrk_lib_ab.py,
+  // interleaved A/B with a float64 check of 64 sampled columns, tools/ab.py syrk,
   // profiles/r05z_syrk_flush_ab.log: config-3 shard 8192 -> 16384 rows 314.2 -> 308.6
   // ms, max error / max|S| 7.0e-7 -> 8.0e-7; config 2 4096 -> 8192 26.58 -> 25.78 ms,
   // 1.9e-7 -> 4.2e-7; 32768 rows at config 3: 305.8 ms but 1.4e-6, config 5's

@@ -153,6 +153,7 @@ class SlaveNode(Node):
                 self._stream = torch.cuda.Stream(batch.device)
             # the rows were uploaded (or written) on the current stream
             self._stream.wait_stream(torch.cuda.current_stream(batch.device))
+            batch.record_stream(self._stream)  # an uploaded copy is freed only after its use
         with (torch.cuda.stream(self._stream) if self._stream is not None else nullcontext()):
             eigenspace = self.compute_sigma_hat_(batch)
             eigenspace = self.top_k_eigenvectors(eigenspace, request["rank"])

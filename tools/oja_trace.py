@@ -34,8 +34,12 @@ for rep in range(3):
 raw = ws.view(torch.uint8)[nbytes - TB:nbytes].cpu().numpy().view(np.uint64).reshape(256, 64, 16)
 tr = raw[:, :nb, :].astype(np.int64)
 names = ["step1 (X wait + MFMA + P stores)", "signal+wait A", "step2 (P loads, T image)", "signal+wait B",
-         "step3 (T load, transposes, Q)", "wait C (wave 7)", "step4 (wave 7)", "-", "wait D"]
-pairs = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6), (6, 7), None, (8, 9)]
+         "step3 (T load, transposes, Q)", "wait C (wave 7)", "step4 (wave 7)", "-", "wait D",
+         "  step3: T fragments land", "  step3: chunk 0 products", "  step3: chunk 0 barrier 1",
+         "  step3: chunk 0 sums, barrier 2, chunk 1 products", "  step3: chunk 1 barrier 1",
+         "  step3: chunk 1 sums + barrier 2"]
+pairs = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6), (6, 7), None, (8, 9),
+         (4, 10), (10, 11), (11, 12), (12, 13), (13, 14), (14, 5)]
 for nm, pr in zip(names, pairs):
     if pr is None:
         continue
