@@ -562,17 +562,6 @@ constexpr int kOjaRedUnroll = DEIG_AB_OJA_RED_UNROLL;
 constexpr int kOjaRedUnroll = 16;
 #endif
 
-// Step 3's transpose of the X block (rows <-> features, through each wave's private LDS
-// region) runs right after step 1, while hand-off A is in flight (r06; before: inside step
-// 3, on the critical path).  The transposed registers are exactly the A operands step 3
-// read back from LDS before, so the products and sums are the same bit for bit.
-// -DDEIG_AB_OJA_LATE_TRANSPOSE: the r05 order (measurement builds only).
-#ifdef DEIG_AB_OJA_LATE_TRANSPOSE
-constexpr bool kOjaEarlyTranspose = false;
-#else
-constexpr bool kOjaEarlyTranspose = true;
-#endif
-
 struct OjaBlk {
   const float* X;  // first batch of the run
   int64_t ldx;
@@ -631,14 +620,6 @@ __device__ __forceinline__ void ob_wait(unsigned* c, unsigned target, unsigned* 
   }
 }
 __device__ __forceinline__ void ob_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// A workgroup barrier for LDS data only: __syncthreads() is a workgroup-scope release
-// too, i.e. an s_waitcnt vmcnt(0) in front of the s_barrier, which in step 3 waited for
-// the next batch's X loads just issued (r06 trace: step 3 took as long as the X stream)
-__device__ __forceinline__ void ob_lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
 
 template <int NB, int NKS>
 __global__ __launch_bounds__(512) void oja_blk_kernel(OjaBlk a) {
@@ -735,35 +716,10 @@ __global__ __launch_bounds__(512) void oja_blk_kernel(OjaBlk a) {
     ob_drain();
     __syncthreads();
     OB_STAMP(1, t == 0);
-    if (t == 0) ob_signal(cA);
-    if constexpr (kOjaEarlyTranspose) {
-      // this wave's X block, k-step by k-step, through its own LDS region: xr[f2][ks][h]
-      // becomes feature 32 ks + 16 f2 + (lane & 15), rows 8 (lane >> 4) + 4 h .. + 3 -
-      // step 3's A operands (no barrier: the region is the wave's own)
-      float* T = xt[wave];
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-          for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              T[(8 * (lane >> 4) + 4 * h + e) * OB_TS + 16 * r + (lane & 15)] = xr[r][ks][h][e];
-        f32x4 q[2][2];
-#pragma unroll
-        for (int f2 = 0; f2 < 2; ++f2) {
-          q[f2][0] = *reinterpret_cast<const f32x4*>(T + (16 * f2 + (lane & 15)) * OB_TS + 8 * (lane >> 4));
-          q[f2][1] = *reinterpret_cast<const f32x4*>(T + (16 * f2 + (lane & 15)) * OB_TS + 8 * (lane >> 4) + 4);
-        }
-#pragma unroll
-        for (int f2 = 0; f2 < 2; ++f2) {
-          xr[f2][ks][0] = q[f2][0];
-          xr[f2][ks][1] = q[f2][1];
-        }
-      }
+    if (t == 0) {
+      ob_signal(cA);
+      ob_wait(cA, target, a.err);
     }
-    if (t == 0) ob_wait(cA, target, a.err);
     __syncthreads();
     OB_STAMP(2, t == 0);
     // ---- 2. T rows R0 + 16 j .. + 15 = sum_j' P_ij'
@@ -822,36 +778,22 @@ __global__ __launch_bounds__(512) void oja_blk_kernel(OjaBlk a) {
 #pragma unroll
         for (int kc = 0; kc < CH / 2; ++kc) {
           const int ks = c0 / 2 + kc;
-          f32x4 xa[2][2];  // step 3's A operands of k-step ks (feature tiles 2 ks, 2 ks + 1)
-          if constexpr (kOjaEarlyTranspose) {
+          // this wave's 32 rows x 32 features of k-step ks, transposed: T[f][row]
 #pragma unroll
-            for (int f2 = 0; f2 < 2; ++f2) {
-              xa[f2][0] = xr[f2][ks][0];
-              xa[f2][1] = xr[f2][ks][1];
-            }
-          } else {
-            // this wave's 32 rows x 32 features of k-step ks, transposed: T[f][row]
+          for (int r = 0; r < 2; ++r)
 #pragma unroll
-            for (int r = 0; r < 2; ++r)
+            for (int h = 0; h < 2; ++h)
 #pragma unroll
-              for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                  T[(8 * (lane >> 4) + 4 * h + e) * OB_TS + 16 * r + (lane & 15)] = xr[r][ks][h][e];
-#pragma unroll
-            for (int f2 = 0; f2 < 2; ++f2) {
-              xa[f2][0] = *reinterpret_cast<const f32x4*>(T + (16 * f2 + (lane & 15)) * OB_TS + 8 * (lane >> 4));
-              xa[f2][1] = *reinterpret_cast<const f32x4*>(T + (16 * f2 + (lane & 15)) * OB_TS + 8 * (lane >> 4) + 4);
-            }
-          }
+              for (int e = 0; e < 4; ++e)
+                T[(8 * (lane >> 4) + 4 * h + e) * OB_TS + 16 * r + (lane & 15)] = xr[r][ks][h][e];
           // waves 0-5: this k-step of the next batch's block streams from here on (its
           // registers are free once staged); waves 6, 7 publish Q and run step 4
-          // first, and their drains would wait for it.  Early transpose: after this
-          // k-step's products (its registers are the operands)
-          if (!kOjaEarlyTranspose && wave < 6 && more) load_x_ks(bt + 1, ks);
+          // first, and their drains would wait for it
+          if (wave < 6 && more) load_x_ks(bt + 1, ks);
 #pragma unroll
           for (int f2 = 0; f2 < 2; ++f2) {
-            const f32x4 a0 = xa[f2][0], a1 = xa[f2][1];
+            const f32x4 a0 = *reinterpret_cast<const f32x4*>(T + (16 * f2 + (lane & 15)) * OB_TS + 8 * (lane >> 4));
+            const f32x4 a1 = *reinterpret_cast<const f32x4*>(T + (16 * f2 + (lane & 15)) * OB_TS + 8 * (lane >> 4) + 4);
             bf16x8 ahi, alo;
             split8(a0, a1, ahi, alo);
 #pragma unroll
@@ -863,14 +805,13 @@ __global__ __launch_bounds__(512) void oja_blk_kernel(OjaBlk a) {
               acc[2 * kc + f2][nb] = c;
             }
           }
-          if (kOjaEarlyTranspose && wave < 6 && more) load_x_ks(bt + 1, ks);
         }
 #pragma unroll
         for (int ft = 0; ft < CH; ++ft)
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb) red[wave][ft][nb][lane] = acc[ft][nb];
         OB_STAMP(11 + 2 * (c0 / CH), t == 0 && c0 / CH < 2);
-        if constexpr (kOjaEarlyTranspose) ob_lds_barrier(); else __syncthreads();
+        __syncthreads();
         OB_STAMP(12 + 2 * (c0 / CH), t == 0 && c0 / CH < 2);
         for (int u = t - 384; u >= 0 && u < CH * NB * 64; u += 128) {  // waves 6, 7
           const int ln = u & 63, nb = (u >> 6) % NB, ft = (u >> 6) / NB;
@@ -881,7 +822,7 @@ __global__ __launch_bounds__(512) void oja_blk_kernel(OjaBlk a) {
           const int col = 16 * nb + (ln & 15);
           ob_st(rq, (uint32_t)((((int64_t)i * (d / 4) + fq) * KP + col) * 16), __builtin_bit_cast(u32x4, sm));
         }
-        if constexpr (kOjaEarlyTranspose) ob_lds_barrier(); else __syncthreads();
+        __syncthreads();
       }
     }
     OB_STAMP(5, t == 0);
@@ -889,10 +830,6 @@ __global__ __launch_bounds__(512) void oja_blk_kernel(OjaBlk a) {
       // Q published by waves 6, 7 only: both drained, the second to arrive signals
       ob_drain();
       if (lane == 0 && atomicAdd(&step3_done, 1u) == 1u) ob_signal(cC);
-      // this wave's block of the next batch streams while hand-off C is in flight (r06;
-      // before: after step 4): step 4's loads return behind it, and by its drain the
-      // block has landed
-      if (kOjaEarlyTranspose && more) load_x(bt + 1);
       // ---- 4. (waves 6, 7) V[F_j] group of 8 features g = i + 16 (wave - 6) (< FB / 8)
       if (lane == 0) ob_wait(cC, target, a.err);
       __builtin_amdgcn_wave_barrier();
@@ -940,7 +877,7 @@ __global__ __launch_bounds__(512) void oja_blk_kernel(OjaBlk a) {
       ob_drain();
       OB_STAMP(7, lane == 0 && wave == 7);
       if (lane == 0 && atomicAdd(&step4_done, 1u) == 1u) ob_signal(cD);
-      if (!kOjaEarlyTranspose && more) load_x(bt + 1);
+      if (more) load_x(bt + 1);
     }
     OB_STAMP(8, t == 0);
     if (more) {
