@@ -188,7 +188,7 @@ def test_c3_server_leg_m8_golden(cuda):
     from tests.conftest import load_golden
     g = load_golden("spiked_d8192_k64_m8_seeded")
     k, m = int(g["k"]), int(g["m"])
-    X = torch.from_numpy(g["Xq"]).to(cuda).float() / float(g["grid"])
+    X = torch.from_numpy(np.array(g["Xq"])).to(cuda).float() / float(g["grid"])
     est = DistributedEigenspaceEstimator(k, workers_per_rank=m)
     r = est.fit(X)
     torch.cuda.synchronize()
