@@ -1586,6 +1586,7 @@ int deig_sym_power_f32(const float* S, int64_t d, int64_t lds, float* Q, int p, 
   step.tau = 0.f;
   step.next_mode = smode;
   for (int i = 0; i < steps; ++i) {
+    step.write_y = i + 1 == steps;  // the contract: on return Y = S Q_{steps-1}
     const int rc = sweep_apply(Q, d, p, ldq, Y, ldy, 1.f, ws, ws_bytes, st, smode, &step, i > 0);
     if (rc) return rc;
   }

@@ -150,6 +150,8 @@ struct SweepStep {
   float tau;                // power: live if cs_j > 0 and |lam_j| >= tau |lam_0|
   float thr, a, cc, gamma;  // Chebyshev: X_{j+1} = a (Y - cc X_j) - gamma X_{j-1} if lam_j >= thr
   int next_mode;            // kSweep* of the next sweep
+  int write_y;              // 1: also store Y = alpha S Q (split-K sums); 0: Y is dead (the
+                            // solver's intermediate sweeps: only the basis step reads it)
 };
 // Several problems of the same d, p and mode in one launch per kernel (solve_batch):
 // problem i's Q, Y, workspace and step buffers sit off[i] bytes after problem 0's

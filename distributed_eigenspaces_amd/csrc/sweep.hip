@@ -658,7 +658,10 @@ __global__ __launch_bounds__(256) void sweep_finish_kernel(const float* __restri
             if (k0 + k < ks) y += v[k];
         }
         y *= alpha;
-        *reinterpret_cast<f32x4*>(Y + r * ldy + c4) = y;
+#ifdef DEIG_AB_SWEEP_ALWAYS_Y
+        st.write_y = 1;  // measurement builds: the r05 behaviour (every sweep stores Y)
+#endif
+        if (st.write_y) *reinterpret_cast<f32x4*>(Y + r * ldy + c4) = y;
       } else {
         y = *reinterpret_cast<const f32x4*>(Y + r * ldy + c4);
       }

@@ -34,7 +34,7 @@ def build(macros, out):
     _build.build_library()
     objdir = os.path.join(_build.HERE, "build")
     hipcc = _build._hipcc()
-    defs = ["-D" + m.lstrip("-D") for m in macros.split()]
+    defs = ["-D" + (m[2:] if m.startswith("-D") else m) for m in macros.split()]
     names = [d[2:].split("=")[0] for d in defs]
     os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
     objs = []
