@@ -390,6 +390,10 @@ class StatusPool {
     free_.clear();
     (void)hipGetLastError();
   }
+  bool empty() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return free_.empty();
+  }
 
  private:
   std::mutex mu_;
@@ -1324,6 +1328,8 @@ extern "C" {
 int deig_version(void) { return 0x000600; }
 
 void deig_shutdown(void) {
+  // nothing allocated (no solver ran in this process): make no HIP call at all
+  if (status_pool().empty()) return;
   (void)hipDeviceSynchronize();
   status_pool().drain();
   (void)hipGetLastError();
