@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 from oracle import ref_cpu
-from tests.conftest import golden_d, golden_names, load_golden
+from tests.conftest import golden_names, load_golden
 
 pytestmark = pytest.mark.gpu
 P_TOL, EV_TOL = 5e-5, 5e-6

@@ -5,7 +5,6 @@ Tolerances: ||P_gpu - P_ref||_F <= 1e-4, eigenvalues <= 1e-5 relative
 (BASELINE.json north_star).  Oja has no reference: parity unpinned, judged by
 sin(theta) against the one-shot oracle."""
 import json
-import threading
 
 import numpy as np
 import pytest

@@ -1,7 +1,7 @@
 """Debug probe: the world-2 streaming-Oja aggregation, in one process."""
 import sys, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import numpy as np, torch, warnings
+import numpy as np, torch
 import distributed_eigenspaces_amd as de
 from tests.test_gpu_distributed import _oja_data
 world, nb, b, d, k, agg = 2, 6, 1024, 256, 6, 3
