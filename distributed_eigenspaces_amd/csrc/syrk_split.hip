@@ -660,9 +660,24 @@ __device__ __forceinline__ void rem_item(const SSched& s, int L, int u, int& til
 // the segment the counts shrink with the pieces not issued.  WAR: every L part
 // retires its reads (lgkmcnt(0)) before its closing barrier.  Same MFMA order per
 // accumulator as the other variants (bit-identical sums).
-template <int PRIO>
+// DW >= 0: a wave of a DIAGONAL tile whose 128 x 64 block starts DW = 64 wj - 128 wi
+// columns right of the diagonal (0, 64 or 128; the other waves of the tile run DW = -1).
+// store4 keeps only i >= j there, so the 16 x 16 MFMA blocks that lie wholly above the
+// diagonal (dw_skip) are neither computed nor their operands read: all of waves 2 and
+// 3 (DW = 128: they only stage their DMA pieces and pass the barriers), 22 of 32 blocks
+// of waves 1 and 7, 6 of waves 0 and 6 - 120 of the tile's 256, MFMAs a power-held
+// chip does not spend.  Every stored sum is the same MFMA chain as before
+// (bit-identical); separate instantiations, so the other tiles' code is unchanged (a
+// runtime test inside the loop measured slower, r06).
+constexpr bool dw_skip(int dw, int mb, int nb) { return dw >= 0 && 16 * mb + 15 < dw + 16 * nb; }
+constexpr bool dw_row(int dw, int mb) { return !dw_skip(dw, mb, 0); }  // A block row mb is read
+constexpr bool dw_col(int dw, int nb) { return !dw_skip(dw, 7, nb); }  // B block column nb is read
+constexpr bool dw_idle(int dw) { return !dw_row(dw, 7); }
+
+template <int PRIO, int DW>
 __device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, int tile, int64_t k0,
                                           int64_t k1, int slot, bool partial, const PaceSeq& pc) {
+  constexpr bool idle = dw_idle(DW);
   constexpr int BUF_B = Geo<2>::BUF_B;
   constexpr int QB = 8 * 1024;  // one A quarter
   constexpr int BOFF = 4 * QB;  // the B panel
@@ -754,7 +769,7 @@ __device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, i
             }
           }
           if (since == s.flush_kt) {
-            flush<16>(slab, !flushed, acc, wave, lane);
+            if constexpr (!idle) flush<16>(slab, !flushed, acc, wave, lane);
             wait_vm<0>();
             flushed = true;
             since = 0;
@@ -767,8 +782,10 @@ __device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, i
           }
 #pragma unroll
           for (int nb = 0; nb < 4; ++nb) {
-            bhi[nb] = *reinterpret_cast<const bf16x8*>(pb + (16 * nb) * 16);
-            blo[nb] = *reinterpret_cast<const bf16x8*>(pb + (BT + 16 * nb) * 16);
+            if (dw_col(DW, nb)) {
+              bhi[nb] = *reinterpret_cast<const bf16x8*>(pb + (16 * nb) * 16);
+              blo[nb] = *reinterpret_cast<const bf16x8*>(pb + (BT + 16 * nb) * 16);
+            }
           }
         } else if (has2) {
           issue_b(k0 + t + 2, cur, 0, 2);
@@ -778,8 +795,10 @@ __device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, i
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const int q = 2 * h + (m >> 1), mm = m & 1;
-          ahi[m] = *reinterpret_cast<const bf16x8*>(pa + q * QB + (16 * mm) * 16);
-          alo[m] = *reinterpret_cast<const bf16x8*>(pa + q * QB + (64 + 16 * mm) * 16);
+          if (dw_row(DW, 4 * h + m)) {
+            ahi[m] = *reinterpret_cast<const bf16x8*>(pa + q * QB + (16 * mm) * 16);
+            alo[m] = *reinterpret_cast<const bf16x8*>(pa + q * QB + (64 + 16 * mm) * 16);
+          }
         }
         if (h == 0) {
           if (has1) wait_vm<8>(); else wait_vm<0>();
@@ -795,13 +814,16 @@ __device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, i
           const int mb = 4 * h + m;
 #pragma unroll
           for (int nb = 0; nb < 4; ++nb)
-            acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[m], bhi[nb], acc.a[mb][nb], 0, 0, 0);
+            if (!dw_skip(DW, mb, nb))
+              acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[m], bhi[nb], acc.a[mb][nb], 0, 0, 0);
 #pragma unroll
           for (int nb = 0; nb < 4; ++nb)
-            acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[m], blo[nb], acc.a[mb][nb], 0, 0, 0);
+            if (!dw_skip(DW, mb, nb))
+              acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[m], blo[nb], acc.a[mb][nb], 0, 0, 0);
 #pragma unroll
           for (int nb = 0; nb < 4; ++nb)
-            acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[m], bhi[nb], acc.a[mb][nb], 0, 0, 0);
+            if (!dw_skip(DW, mb, nb))
+              acc.a[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[m], bhi[nb], acc.a[mb][nb], 0, 0, 0);
         }
         if (PRIO) __builtin_amdgcn_s_setprio(0);
         bar();
@@ -809,13 +831,14 @@ __device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, i
     }
     if (!lag) bar();  // balance the stagger
   }
-  if (flushed) unflush<16>(slab, acc, wave, lane);
+  if (flushed && !idle) unflush<16>(slab, acc, wave, lane);
   if (partial) {
 #pragma unroll
     for (int q = 0; q < NQUAD; ++q)
       *slab_at(slab, wave, q, lane) = f32x4{acc.at(q, 0), acc.at(q, 1), acc.at(q, 2), acc.at(q, 3)};
     return;
   }
+  if constexpr (idle) return;
 #pragma unroll
   for (int q = 0; q < NQUAD; ++q) {
     const float a[4] = {acc.at(q, 0), acc.at(q, 1), acc.at(q, 2), acc.at(q, 3)};
@@ -868,7 +891,20 @@ __global__ __launch_bounds__(NTHR) void syrks_h_kernel(SSched s) {
 #endif
       }
     }
-    segment_h<PRIO>(s, lds, tile, k0, k1, slot, partial, pc);
+    const int tt = __builtin_amdgcn_readfirstlane(s.order[tile]);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool dg = (tt & 0xffff) == (tt >> 16);
+#ifndef DEIG_AB_SYRK_NO_DIAG_IDLE
+    const int dw = 64 * (wv & 3) - 128 * (wv >> 2);
+    if (dg && dw == 0)
+      segment_h<PRIO, 0>(s, lds, tile, k0, k1, slot, partial, pc);
+    else if (dg && dw == 64)
+      segment_h<PRIO, 64>(s, lds, tile, k0, k1, slot, partial, pc);
+    else if (dg && dw == 128)
+      segment_h<PRIO, 128>(s, lds, tile, k0, k1, slot, partial, pc);
+    else
+#endif
+      segment_h<PRIO, -1>(s, lds, tile, k0, k1, slot, partial, pc);
   }
 }
 
