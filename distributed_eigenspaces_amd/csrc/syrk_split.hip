@@ -660,8 +660,14 @@ __device__ __forceinline__ void rem_item(const SSched& s, int L, int u, int& til
 // the segment the counts shrink with the pieces not issued.  WAR: every L part
 // retires its reads (lgkmcnt(0)) before its closing barrier.  Same MFMA order per
 // accumulator as the other variants (bit-identical sums).
-// DW >= 0: a wave of a DIAGONAL tile whose 128 x 64 block starts DW = 64 wj - 128 wi
-// columns right of the diagonal (0, 64 or 128; the other waves of the tile run DW = -1).
+// DW != -1: a DIAGONAL tile.  Its B panel is its A panel, so no B pieces are staged
+// and the B operands are read from the A quarters (the same bytes in the A layout);
+// with 2 DMA pieces per L part instead of 4 the counted waits become 4 / 2, and the end
+// of L_1 also waits for quarters 2, 3 of the next K-tile (phase 0 reads them as B).
+// The same B-operand read point and restage points as before, so the WAR argument
+// above holds unchanged.
+// DW >= 0: a wave of a diagonal tile whose 128 x 64 block starts DW = 64 wj - 128 wi
+// columns right of the diagonal (0, 64 or 128; waves 4 and 5 of the tile run DW = -2).
 // store4 keeps only i >= j there, so the 16 x 16 MFMA blocks that lie wholly above the
 // diagonal (dw_skip) are neither computed nor their operands read: all of waves 2 and
 // 3 (DW = 128: they only stage their DMA pieces and pass the barriers), 22 of 32 blocks
@@ -669,6 +675,7 @@ __device__ __forceinline__ void rem_item(const SSched& s, int L, int u, int& til
 // chip does not spend.  Every stored sum is the same MFMA chain as before
 // (bit-identical); separate instantiations, so the other tiles' code is unchanged (a
 // runtime test inside the loop measured slower, r06).
+constexpr int kDwOff = -1, kDwDiag = -2;
 constexpr bool dw_skip(int dw, int mb, int nb) { return dw >= 0 && 16 * mb + 15 < dw + 16 * nb; }
 constexpr bool dw_row(int dw, int mb) { return !dw_skip(dw, mb, 0); }  // A block row mb is read
 constexpr bool dw_col(int dw, int nb) { return !dw_skip(dw, 7, nb); }  // B block column nb is read
@@ -678,6 +685,11 @@ template <int PRIO, int DW>
 __device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, int tile, int64_t k0,
                                           int64_t k1, int slot, bool partial, const PaceSeq& pc) {
   constexpr bool idle = dw_idle(DW);
+#ifndef DEIG_AB_SYRK_DIAG_B_DMA
+  constexpr bool dgb = DW != kDwOff;  // B operands from the A quarters
+#else
+  constexpr bool dgb = false;
+#endif
   constexpr int BUF_B = Geo<2>::BUF_B;
   constexpr int QB = 8 * 1024;  // one A quarter
   constexpr int BOFF = 4 * QB;  // the B panel
@@ -725,14 +737,14 @@ __device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, i
     __syncthreads();  // ... and its last reads of the ring
     // K-tile k0 whole, then K-tile k0 + 1's B parts 0, 1 and quarters 0, 1 (as an
     // L_1 of K-tile k0 - 1 would have issued them)
-    issue_b(k0, lds, 0, 4);
+    if constexpr (!dgb) issue_b(k0, lds, 0, 4);
 #pragma unroll
     for (int q = 0; q < 4; ++q) issue_a(k0, q, lds);
     if (nkt > 1) {
-      issue_b(k0 + 1, lds + BUF_B, 0, 2);
+      if constexpr (!dgb) issue_b(k0 + 1, lds + BUF_B, 0, 2);
       issue_a(k0 + 1, 0, lds + BUF_B);
       issue_a(k0 + 1, 1, lds + BUF_B);
-      wait_vm<4>();  // K-tile k0 landed
+      wait_vm<dgb ? 2 : 4>();  // K-tile k0 landed
     } else {
       wait_vm<0>();
     }
@@ -753,6 +765,9 @@ __device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, i
       const bool has1 = t + 1 < nkt, has2 = t + 2 < nkt;
       const unsigned char* pa = cur + ((g4 * 2) * 64 + 32 * wi + c) * 16;
       const unsigned char* pb = cur + BOFF + ((g4 * 2) * BT + 64 * wj + c) * 16;
+      // B feature f = 64 wj + 16 nb + c of slice 2 g4 (+1: lo) in the A layout:
+      // quarter (f % 128) / 32, lane 32 (f / 128) + f % 32
+      const unsigned char* pbd = cur + (2 * (wj & 1)) * QB + (2 * g4) * 1024 + (32 * (wj >> 1) + c) * 16;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         // ---------------- L part
@@ -776,19 +791,25 @@ __device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, i
           }
           ++since;
           if (has1) {
-            issue_b(k0 + t + 1, nxt, 2, 4);
+            if constexpr (!dgb) issue_b(k0 + t + 1, nxt, 2, 4);
             issue_a(k0 + t + 1, 2, nxt);
             issue_a(k0 + t + 1, 3, nxt);
           }
 #pragma unroll
           for (int nb = 0; nb < 4; ++nb) {
             if (dw_col(DW, nb)) {
-              bhi[nb] = *reinterpret_cast<const bf16x8*>(pb + (16 * nb) * 16);
-              blo[nb] = *reinterpret_cast<const bf16x8*>(pb + (BT + 16 * nb) * 16);
+              if constexpr (dgb) {
+                const unsigned char* pq = pbd + (nb >> 1) * QB + (16 * (nb & 1)) * 16;
+                bhi[nb] = *reinterpret_cast<const bf16x8*>(pq);
+                blo[nb] = *reinterpret_cast<const bf16x8*>(pq + 1024);
+              } else {
+                bhi[nb] = *reinterpret_cast<const bf16x8*>(pb + (16 * nb) * 16);
+                blo[nb] = *reinterpret_cast<const bf16x8*>(pb + (BT + 16 * nb) * 16);
+              }
             }
           }
         } else if (has2) {
-          issue_b(k0 + t + 2, cur, 0, 2);
+          if constexpr (!dgb) issue_b(k0 + t + 2, cur, 0, 2);
           issue_a(k0 + t + 2, 0, cur);
           issue_a(k0 + t + 2, 1, cur);
         }
@@ -800,7 +821,13 @@ __device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, i
             alo[m] = *reinterpret_cast<const bf16x8*>(pa + q * QB + (64 + 16 * mm) * 16);
           }
         }
-        if (h == 0) {
+        if constexpr (dgb) {  // 2 pieces per L part; phase 0 reads all four quarters
+          if (h == 0) {
+            if (has1) wait_vm<4>(); else wait_vm<0>();
+          } else {
+            if (has2) wait_vm<2>(); else wait_vm<0>();
+          }
+        } else if (h == 0) {
           if (has1) wait_vm<8>(); else wait_vm<0>();
         } else {
           if (has2) wait_vm<6>(); else if (has1) wait_vm<2>(); else wait_vm<0>();
@@ -902,9 +929,11 @@ __global__ __launch_bounds__(NTHR) void syrks_h_kernel(SSched s) {
       segment_h<PRIO, 64>(s, lds, tile, k0, k1, slot, partial, pc);
     else if (dg && dw == 128)
       segment_h<PRIO, 128>(s, lds, tile, k0, k1, slot, partial, pc);
+    else if (dg)
+      segment_h<PRIO, kDwDiag>(s, lds, tile, k0, k1, slot, partial, pc);
     else
 #endif
-      segment_h<PRIO, -1>(s, lds, tile, k0, k1, slot, partial, pc);
+      segment_h<PRIO, kDwOff>(s, lds, tile, k0, k1, slot, partial, pc);
   }
 }
 
