@@ -419,6 +419,7 @@ __device__ __forceinline__ f32x4* slab_at(float* slab, int wave, int q, int lane
 
 // The slab addresses are formed here from an opaque base: otherwise the compiler
 // hoists all 32 of them out of the K loop and keeps 64 VGPRs live for them.
+#ifdef DEIG_AB_SYRK_SERIAL_FLUSH
 template <int MF>
 __device__ __forceinline__ void flush(float* slab, bool first, Acc<MF>& acc, int wave, int lane) {
   asm volatile("" : "+v"(slab));
@@ -432,16 +433,79 @@ __device__ __forceinline__ void flush(float* slab, bool first, Acc<MF>& acc, int
     for (int u = 0; u < 4; ++u) acc.set(q, u, 0.f);
   }
 }
+#else
+// r06: buffer loads / stores in batches of kFlushBatch quads.  Through a generic
+// pointer the slab accesses were flat_* operations, which the hardware may complete
+// out of order, so each quad's read was its own vmcnt(0) round trip: 32 serial round
+// trips per flush (~34 us per event at config 3).  Buffer operations complete in issue
+// order, so a batch's reads are in flight together (its write-backs stay queued
+// behind them).
+#ifdef DEIG_AB_SYRK_FLUSH_BATCH
+constexpr int kFlushBatch = DEIG_AB_SYRK_FLUSH_BATCH;
+#else
+constexpr int kFlushBatch = 4;
+#endif
+template <int MF>
+__device__ __forceinline__ void flush(float* slab, bool first, Acc<MF>& acc, int wave, int lane) {
+  asm volatile("" : "+v"(slab));
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(slab, (short)0, (int)(SLAB * sizeof(float)), 0x00020000);
+  const int voff = (wave * NQUAD * 64 + lane) * 16;
+  auto put = [&](int q, f32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff + q * 1024, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc.set(q, u, 0.f);
+  };
+  if (first) {
+#pragma unroll
+    for (int q = 0; q < NQUAD; ++q) put(q, f32x4{acc.at(q, 0), acc.at(q, 1), acc.at(q, 2), acc.at(q, 3)});
+    return;
+  }
+#pragma unroll
+  for (int b = 0; b < NQUAD; b += kFlushBatch) {
+    f32x4 v[kFlushBatch];
+#pragma unroll
+    for (int i = 0; i < kFlushBatch; ++i)
+      v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff + (b + i) * 1024, 0, 0));
+    __builtin_amdgcn_sched_barrier(0);  // the batch's reads issue together
+#pragma unroll
+    for (int i = 0; i < kFlushBatch; ++i) {
+      const int q = b + i;
+      put(q, v[i] + f32x4{acc.at(q, 0), acc.at(q, 1), acc.at(q, 2), acc.at(q, 3)});
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+#endif
 
 template <int MF>
 __device__ __forceinline__ void unflush(float* slab, Acc<MF>& acc, int wave, int lane) {
   asm volatile("" : "+v"(slab));
+#ifdef DEIG_AB_SYRK_SERIAL_FLUSH
 #pragma unroll
   for (int q = 0; q < NQUAD; ++q) {
     const f32x4 v = *slab_at(slab, wave, q, lane);
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc.set(q, u, acc.at(q, u) + v[u]);
   }
+#else
+  // buffer loads in batches (flat loads were one vmcnt(0) round trip each, see flush)
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(slab, (short)0, (int)(SLAB * sizeof(float)), 0x00020000);
+  const int voff = (wave * NQUAD * 64 + lane) * 16;
+#pragma unroll
+  for (int b = 0; b < NQUAD; b += kFlushBatch) {
+    f32x4 v[kFlushBatch];
+#pragma unroll
+    for (int i = 0; i < kFlushBatch; ++i)
+      v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff + (b + i) * 1024, 0, 0));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < kFlushBatch; ++i)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc.set(b + i, u, acc.at(b + i, u) + v[i][u]);
+  }
+#endif
 }
 
 // Store 4 consecutive rows ib..ib+3 of column j (values = alpha * a[u] (+ S)),
