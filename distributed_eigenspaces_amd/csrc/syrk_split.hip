@@ -115,6 +115,12 @@ struct SSched {
 // all remainder: 24.77 -> 24.54 ms; config 3 286.0 -> 284.8).  Config 5 (short K per
 // tile) is unchanged.
 constexpr int kChipPaceEvery = 2;
+// flush stagger per XCD = flush_kt / kFlushStaggerDiv K-tiles (0: none)
+#ifdef DEIG_AB_SYRK_FLUSH_STAGGER
+constexpr int kFlushStaggerDiv = DEIG_AB_SYRK_FLUSH_STAGGER;
+#else
+constexpr int kFlushStaggerDiv = 16;
+#endif
 
 __device__ __noinline__ void xcd_pace(unsigned* ctr, unsigned target) {
   __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -816,9 +822,13 @@ __device__ __forceinline__ void segment_h(const SSched& s, unsigned char* lds, i
     bar();
     if (lag) bar();  // the stagger
     const int c = lane & 15, g4 = lane >> 4;
-    int since = 0, since_pace = 0, pace_left = pc.n;
-    unsigned pace_t = pc.base;
     const int xcd = blockIdx.x & 7;
+    // Flush stagger (r06): XCD x flushes x * flush_kt / 16 K-tiles earlier than XCD 0,
+    // so the eight XCDs' slab bursts fall at different K-tiles instead of all at once
+    // (each partial sum still spans flush_kt K-tiles, the first one of a segment fewer).
+    int since = kFlushStaggerDiv > 0 ? xcd * (s.flush_kt / kFlushStaggerDiv) : 0;
+    int since_pace = 0, pace_left = pc.n;
+    unsigned pace_t = pc.base;
     int gcount = 0;
     unsigned gtarget = pc.gbase;
     bf16x8 bhi[4], blo[4];
