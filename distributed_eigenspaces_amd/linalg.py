@@ -393,7 +393,8 @@ def topk_eigh_batch(Ss, k: int, *, p: int | None = None, tol: float = DEFAULT_TO
     """``topk_eigh`` of W same-shape symmetric matrices at once (the logical workers
     of one GPU, each SlaveNode's top_k_eigenvectors of distributed.py:22-29,
     :42-53): the same results as W ``topk_eigh`` calls, the W problems advanced in
-    lockstep on the current stream with each step's sweeps, Grams, small
+    lockstep on the current stream (two interleaved groups on a second, joined
+    stream from d = 2048) with each step's sweeps, Grams, small
     Rayleigh-Ritz solves and updates batched across them (include/deig.h
     deig_topk_sym_batch).  Returns a list of EigResult."""
     Ss = [require_device_tensor(S, "topk_eigh_batch", keep_f64=True) for S in Ss]

@@ -274,7 +274,9 @@ int deig_projavg_topk_f32(const float* Wt, int64_t d, int64_t mk, int64_t ldw,
  * is enqueued as batched launches on `stream` (the sweeps of all problems at the same
  * point of their plans in one launch per kernel, one Gram, one small-solve launch of
  * one workgroup per problem, one update) and one stream sync serves every problem's
- * host decisions.  All work is ordered on `stream`.  Workspace:
+ * host decisions; for d >= 2048 the problems run as two interleaved groups, the second
+ * on an internal stream created for the call that waits for `stream` on entry and
+ * that `stream` waits for on return.  All work is ordered on `stream`.  Workspace:
  * deig_topk_batch_workspace(W, ...) bytes.  Returns the first error;
  * DEIG_NOT_CONVERGED if any problem stopped above tol.  status_out[i] (host array,
  * may be NULL): problem i's own return code, the one deig_topk_sym_ex would have
