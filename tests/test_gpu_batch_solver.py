@@ -38,6 +38,31 @@ def test_batch_equals_separate_solves(dtype, cuda):
         assert torch.equal(a.evals, b.evals)
 
 
+def test_batch_two_stream_groups_equal_separate_solves(cuda):
+    """d >= 2048: the batch runs as two interleaved groups on two streams (capi.hip
+    solve_batch, r06); an odd count (groups of 2 and 1) with one dominant-mean problem
+    (deflation path): still bit-identical to separate solves, and everything is
+    ordered on the caller's stream when the call returns."""
+    import distributed_eigenspaces_amd as de
+    d, k = 2048, 12
+    Ss = [_spiked_cov(d, k, 8192, 7 + 3 * i, cuda, mean=(3.0 if i == 1 else 0.0)) for i in range(3)]
+    single = [de.topk_eigh(S, k) for S in Ss]
+    side = torch.cuda.Stream(cuda)
+    side.wait_stream(torch.cuda.current_stream(cuda))
+    with torch.cuda.stream(side):  # a non-default caller stream
+        for S in Ss:
+            S.record_stream(side)
+        batch = de.topk_eigh_batch(Ss, k)
+        checks = [(b.V * 1.0).sum() for b in batch]  # work queued behind the call on `side`
+    side.synchronize()
+    torch.cuda.synchronize(cuda)
+    for a, b, c in zip(single, batch, checks):
+        assert a.sweeps == b.sweeps
+        assert torch.equal(a.V, b.V)
+        assert torch.equal(a.evals, b.evals)
+        assert torch.equal(c, (a.V * 1.0).sum())
+
+
 def test_batch_c1_shape_vs_oracle(cuda):
     """configs[0]'s worker shape: 8 byte shards (6250 x 3072, uncentered, float64
     exact covariance), k = 10, against float64 eigh of each shard."""
