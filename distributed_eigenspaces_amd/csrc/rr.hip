@@ -932,11 +932,13 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
             X1[ar * p + bc] = cr * y1 - sr * w1;
             X1[br * p + bc] = sr * y1 + cr * w1;
           }
+#ifndef DEIG_AB_RR_NO_V  // measurement knock-out only (wrong vectors)
           for (int r = tr0; r < p; r += cpt) {
             const float va = X2[r * p + ac], vb = X2[r * p + bc];
             X2[r * p + ac] = cc * va - sc * vb;
             X2[r * p + bc] = sc * va + cc * vb;
           }
+#endif
         }
 #endif
       }
