@@ -737,7 +737,8 @@ __device__ __forceinline__ void rem_item(const SSched& s, int L, int u, int& til
 // The same B-operand read point and restage points as before, so the WAR argument
 // above holds unchanged.
 // DW >= 0: a wave of a diagonal tile whose 128 x 64 block starts DW = 64 wj - 128 wi
-// columns right of the diagonal (0, 64 or 128; waves 4 and 5 of the tile run DW = -2).
+// columns right of the diagonal (0, 64, or 128 for waves 2 and 3 alike, whose blocks lie
+// wholly above it; waves 4 and 5 of the tile run DW = -2).
 // store4 keeps only i >= j there, so the 16 x 16 MFMA blocks that lie wholly above the
 // diagonal (dw_skip) are neither computed nor their operands read: all of waves 2 and
 // 3 (DW = 128: they only stage their DMA pieces and pass the barriers), 22 of 32 blocks
@@ -1001,7 +1002,7 @@ __global__ __launch_bounds__(NTHR) void syrks_h_kernel(SSched s) {
       segment_h<PRIO, 0>(s, lds, tile, k0, k1, slot, partial, pc);
     else if (dg && dw == 64)
       segment_h<PRIO, 64>(s, lds, tile, k0, k1, slot, partial, pc);
-    else if (dg && dw == 128)
+    else if (dg && dw >= 128)  // waves 2 and 3: the whole block above the diagonal
       segment_h<PRIO, 128>(s, lds, tile, k0, k1, slot, partial, pc);
     else if (dg)
       segment_h<PRIO, kDwDiag>(s, lds, tile, k0, k1, slot, partial, pc);
