@@ -775,16 +775,23 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
   //         moved along the circle method, lower-triangle storage, rotations per wave
   //         by shuffles - their extra VALU / shuffle issue cost more than the LDS
   //         traffic they saved, profiles/r04d_rr_phases.log).
-  //         symmetrise H~; X2 = L^-1 -> the eigenvector accumulator V0 = L^-T
+  //         symmetrise H~; X2 = L^-1 -> the eigenvector accumulator V0 = L^-T, kept
+  //         transposed (X2 = V^T, as L^-1 already is): a column pair's rotation then
+  //         updates two contiguous rows, 4 entries per b128 LDS access (r06: the
+  //         scalar-column V update was ~28 % of a Jacobi step, profiles/r06aq_*)
   for (int idx = tid; idx < pp; idx += NT) {
     const int a = idx / p, b = idx - a * p;
     if (a < b) {
       const float v = 0.5f * (X1[a * p + b] + X1[b * p + a]);
       X1[a * p + b] = v;
       X1[b * p + a] = v;
+#if defined(DEIG_AB_RR_JOLD) || defined(DEIG_AB_RR_VROW)
       const float l = X2[b * p + a];
       X2[a * p + b] = l;
       X2[b * p + a] = 0.f;
+#else
+      X2[a * p + b] = 0.f;
+#endif
     }
   }
   if (tid == 0) {
@@ -797,6 +804,14 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
   const int dq = NT / half, dr = NT - dq * half;
 #else
   const int cpt = NT / half;
+#ifndef DEIG_AB_RR_VROW
+  // V^T items: (column pair t, quad q of its two rows), t-major so that a wave's lanes
+  // walk contiguous quads of one row pair
+  const int vnq = p >> 2;
+  // (counted from the last thread: at small p the first waves carry the H~ update)
+  const int vt0 = (NT - 1 - tid) / vnq, vq0 = (NT - 1 - tid) - vt0 * vnq;
+  const int vdt = NT / vnq, vdq = NT - vdt * vnq;
+#endif
 #endif
   for (int sw = 0; sw < max_jsweeps; ++sw) {
     if (tid == 0) nrot[0] = 0;
@@ -932,7 +947,7 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
             X1[ar * p + bc] = cr * y1 - sr * w1;
             X1[br * p + bc] = sr * y1 + cr * w1;
           }
-#ifndef DEIG_AB_RR_NO_V  // measurement knock-out only (wrong vectors)
+#if defined(DEIG_AB_RR_VROW) && !defined(DEIG_AB_RR_NO_V)  // r05 layout (measurement builds)
           for (int r = tr0; r < p; r += cpt) {
             const float va = X2[r * p + ac], vb = X2[r * p + bc];
             X2[r * p + ac] = cc * va - sc * vb;
@@ -940,6 +955,29 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
           }
 #endif
         }
+#if !defined(DEIG_AB_RR_VROW) && !defined(DEIG_AB_RR_NO_V)  // NO_V: knock-out, wrong vectors
+        for (int t = vt0, q = vq0; t < half;) {
+          const f32x4 qc = rotp[t];
+          const float cc = qc[0], sc = qc[1];
+          f32x4* pa = reinterpret_cast<f32x4*>(X2 + __float_as_int(qc[2]) * p) + q;
+          f32x4* pb = reinterpret_cast<f32x4*>(X2 + __float_as_int(qc[3]) * p) + q;
+          const f32x4 va = *pa, vb = *pb;
+          f32x4 na, nb;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            na[e] = cc * va[e] - sc * vb[e];
+            nb[e] = sc * va[e] + cc * vb[e];
+          }
+          *pa = na;
+          *pb = nb;
+          t += vdt;
+          q += vdq;
+          if (q >= vnq) {
+            q -= vnq;
+            ++t;
+          }
+        }
+#endif
 #endif
       }
       __syncthreads();
@@ -969,6 +1007,23 @@ __device__ __forceinline__ void rr_small2_body(const float* __restrict__ Cg, int
   stamp(7);
   // ---- 5. eigenvalues; W = D (L^-T U) in X2 (row scaling in place); X1 = scratch
   for (int a = tid; a < p; a += NT) lamv[a] = X1[a * p + a];
+#if !defined(DEIG_AB_RR_JOLD) && !defined(DEIG_AB_RR_VROW)
+  for (int it = tid; it < nt4 * (nt4 + 1) / 2; it += NT) {  // V^T -> V by 4 x 4 blocks
+    int ti, tj;
+    tri_rc(it, ti, tj);
+    f32x4 A[4], B[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      A[r] = *reinterpret_cast<const f32x4*>(X2 + (4 * ti + r) * p + 4 * tj);
+      B[r] = *reinterpret_cast<const f32x4*>(X2 + (4 * tj + r) * p + 4 * ti);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      *reinterpret_cast<f32x4*>(X2 + (4 * ti + r) * p + 4 * tj) = f32x4{B[0][r], B[1][r], B[2][r], B[3][r]};
+      *reinterpret_cast<f32x4*>(X2 + (4 * tj + r) * p + 4 * ti) = f32x4{A[0][r], A[1][r], A[2][r], A[3][r]};
+    }
+  }
+#endif
   __syncthreads();
   for (int idx = tid; idx < pp; idx += NT) X2[idx] *= dsc[idx / p];
   float* Wm = X2;   // W = D L^-T U

@@ -213,7 +213,7 @@ def ab_oja(reps, orth, paths):
 
 # ---------------------------------------------------------------- rr phases
 RR_CHILD = r'''
-import os, sys
+import hashlib, os, sys
 sys.path.insert(0, os.environ["DEIG_ROOT"])
 import torch
 import distributed_eigenspaces_amd as de
@@ -227,7 +227,9 @@ for name, n, d, k in (("c1", 6250, 3072, 10), ("c3", 16384, 8192, 64), ("c5", 32
     print(f"=== {name}", file=sys.stderr, flush=True)
     r = de.topk_eigh(S, k, check_finite=False)
     torch.cuda.synchronize()
-    print(f"=== {name} done sweeps {r.sweeps} resid {r.resid:.3e} conv {r.converged}", file=sys.stderr, flush=True)
+    h = hashlib.sha1(r.V.cpu().numpy().tobytes() + r.evals.cpu().numpy().tobytes()).hexdigest()[:12]
+    print(f"=== {name} done sweeps {r.sweeps} resid {r.resid:.3e} conv {r.converged} out {h}", file=sys.stderr,
+          flush=True)
     del S
     torch.cuda.empty_cache()
 '''
