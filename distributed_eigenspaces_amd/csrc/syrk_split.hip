@@ -1376,10 +1376,20 @@ void launch_split_pass_kernel(int G, hipStream_t stream, const SSched& s) {
 
 }  // namespace
 
+// Persistent grid: one block per CU (measurement builds may set a smaller grid, for a
+// stream whose CU mask leaves the rest of the chip to other work)
+int syrk_cus() {
+#ifdef DEIG_AB_SYRK_G
+  return DEIG_AB_SYRK_G;
+#else
+  return num_cus();
+#endif
+}
+
 size_t syrk_split_workspace_bytes(int64_t n, int64_t d) {
   if (n < 1 || d < 1) return 0;
-  if (syrk_variant(d) == 163) return make_layout(n, d, num_cus(), 0).total;
-  return make_layout(n, d, num_cus(), default_chunk_rows(n, d)).total;
+  if (syrk_variant(d) == 163) return make_layout(n, d, syrk_cus(), 0).total;
+  return make_layout(n, d, syrk_cus(), default_chunk_rows(n, d)).total;
 }
 
 int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float alpha, float* S,
@@ -1391,7 +1401,7 @@ int syrk_split_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float a
   DEIG_REQUIRE(ldx >= d && ldx % 4 == 0, "syrk: ldx must be >= d and a multiple of 4");
   DEIG_REQUIRE(lds >= d && lds % 4 == 0, "syrk: lds must be >= d and a multiple of 4");
   DEIG_REQUIRE(X && S && aligned16(X) && aligned16(S), "syrk: X and S must be 16-byte aligned");
-  const int G = num_cus();
+  const int G = syrk_cus();
   const int variant = syrk_variant(d);
   const bool fused = variant == 163;
   // Largest chunk (multiple of 32 rows, <= n rounded up) that fits the workspace.
