@@ -35,6 +35,7 @@ DEIG_SWEEP_FP32 = 2
 DEIG_SWEEP_PREPARED = 0x100
 DEIG_SWEEP_ROUND_Q = 0x200
 DEIG_SWEEP_FAST = 0x400
+DEIG_SWEEP_HALF = 0x1000
 DEIG_SWEEP_KERNEL_ONLY = 0x800
 SWEEP_ALGOS = {"auto": DEIG_SWEEP_AUTO, "bf16x6": DEIG_SWEEP_BF16X6, "fp32": DEIG_SWEEP_FP32}
 DEIG_U8_RAW = 0
@@ -64,6 +65,7 @@ class SolverOpts(ctypes.Structure):
         ("fast_until", ctypes.c_float),
         ("round_until", ctypes.c_float),
         ("debug", ctypes.c_int),
+        ("half_until", ctypes.c_float),
     ]
 
 _c_i64 = ctypes.c_int64

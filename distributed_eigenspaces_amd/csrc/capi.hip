@@ -102,6 +102,7 @@ struct Opts {
   float jcap_above = -1.f;
   float fast_until = 1e-3f;
   float round_until = 1e-4f;
+  float half_until = 1e-2f;
   bool debug = false;
 };
 
@@ -118,6 +119,7 @@ Opts make_opts(const deig_solver_opts* o) {
   r.jcap_above = o->jacobi_early_above;
   r.fast_until = o->fast_until;
   r.round_until = o->round_until;
+  r.half_until = o->half_until;
   r.debug = o->debug != 0;
   return r;
 }
@@ -542,7 +544,8 @@ struct Solver {
     // then Q rounded to two pieces (five products) down to round_until; the
     // closing sweeps exact (the rounding puts ~4e-6 relative noise into the basis
     // each sweep: a floor under the residual).
-    const int smode = (o.fast_until > 0.f && last > fmaxf(o.fast_until, tol)) ? kSweepFast
+    const int smode = (o.half_until > 0.f && last > fmaxf(o.half_until, tol))     ? kSweepHalf
+                      : (o.fast_until > 0.f && last > fmaxf(o.fast_until, tol)) ? kSweepFast
                       : last > fmaxf(o.round_until, tol)                      ? kSweepRoundQ
                                                                               : kSweepExact;
     ChebPlan cp;
@@ -1406,6 +1409,7 @@ void deig_solver_opts_init(deig_solver_opts* o) {
   o->fast_until = 1e-3f;
   o->round_until = 1e-4f;
   o->debug = 0;
+  o->half_until = 1e-2f;
 }
 
 // An explicit S the solver reads in place needs lds % 4 == 0 and 16-byte alignment;
@@ -1626,10 +1630,11 @@ int deig_sym_power_f32(const float* S, int64_t d, int64_t lds, float* Q, int p, 
   g_err[0] = 0;
   DEIG_REQUIRE(steps >= 1 && cs && Q, "sym_power: need steps >= 1, cs and Q");
   const bool prepared = (algo & DEIG_SWEEP_PREPARED) != 0;
-  const int smode = (algo & DEIG_SWEEP_FAST)      ? kSweepFast
+  const int smode = (algo & DEIG_SWEEP_HALF)      ? kSweepHalf
+                    : (algo & DEIG_SWEEP_FAST)    ? kSweepFast
                     : (algo & DEIG_SWEEP_ROUND_Q) ? kSweepRoundQ
                                                   : kSweepExact;
-  algo &= ~(DEIG_SWEEP_PREPARED | DEIG_SWEEP_ROUND_Q | DEIG_SWEEP_FAST);
+  algo &= ~(DEIG_SWEEP_PREPARED | DEIG_SWEEP_ROUND_Q | DEIG_SWEEP_FAST | DEIG_SWEEP_HALF);
   if (algo != DEIG_SWEEP_AUTO && algo != DEIG_SWEEP_BF16X6)
     return fail(DEIG_EINVAL, "sym_power: algorithm %d has no fused chain (bf16x6 only)", algo);
   hipStream_t st = (hipStream_t)stream;
@@ -1654,7 +1659,8 @@ int deig_sym_power_f32(const float* S, int64_t d, int64_t lds, float* Q, int p, 
 }
 
 size_t deig_sym_apply_workspace(int64_t d, int p, int algo) {
-  algo &= ~(DEIG_SWEEP_PREPARED | DEIG_SWEEP_ROUND_Q | DEIG_SWEEP_FAST | DEIG_SWEEP_KERNEL_ONLY);
+  algo &= ~(DEIG_SWEEP_PREPARED | DEIG_SWEEP_ROUND_Q | DEIG_SWEEP_FAST | DEIG_SWEEP_HALF |
+            DEIG_SWEEP_KERNEL_ONLY);
   if (algo == DEIG_SWEEP_FP32) return skinny_workspace_bytes(d, p, d);
   return sweep_workspace_bytes(d, p);
 }
@@ -1668,10 +1674,12 @@ int deig_sym_apply_f32(const float* S, int64_t d, int64_t lds, const float* Q, i
                          static_cast<float*>(ws), ws_bytes, (hipStream_t)stream);
   const bool prepared = (algo & DEIG_SWEEP_PREPARED) != 0;
   const bool kernel_only = (algo & DEIG_SWEEP_KERNEL_ONLY) != 0;
-  const int smode = (algo & DEIG_SWEEP_FAST)      ? kSweepFast
+  const int smode = (algo & DEIG_SWEEP_HALF)      ? kSweepHalf
+                    : (algo & DEIG_SWEEP_FAST)    ? kSweepFast
                     : (algo & DEIG_SWEEP_ROUND_Q) ? kSweepRoundQ
                                                   : kSweepExact;
-  algo &= ~(DEIG_SWEEP_PREPARED | DEIG_SWEEP_ROUND_Q | DEIG_SWEEP_FAST | DEIG_SWEEP_KERNEL_ONLY);
+  algo &= ~(DEIG_SWEEP_PREPARED | DEIG_SWEEP_ROUND_Q | DEIG_SWEEP_FAST | DEIG_SWEEP_HALF |
+            DEIG_SWEEP_KERNEL_ONLY);
   if (algo != DEIG_SWEEP_AUTO && algo != DEIG_SWEEP_BF16X6)
     return fail(DEIG_EINVAL, "sym_apply: unknown algorithm %d", algo);
   if (!prepared) {

@@ -134,7 +134,7 @@ int sweep_prepare(const void* S, int stype, int64_t d, int64_t lds, int p, void*
 // (sweep.hip split_q_kernel).  mode 2 (early sweeps): as 1, and S is taken as its
 // two leading bf16 pieces from the prepared two-piece image - three products, no
 // split in the sweep, ~2^-16 relative.
-constexpr int kSweepExact = 0, kSweepRoundQ = 1, kSweepFast = 2;
+constexpr int kSweepExact = 0, kSweepRoundQ = 1, kSweepFast = 2, kSweepHalf = 3;
 // Optional epilogue of a sweep in the solver's chain, fused with the split-K
 // reduction (sweep_finish_kernel): the basis step that turns Y = S Q into the next
 // Q (the elementwise rr_power_kernel / cheb_step_kernel forms), and the next

@@ -451,7 +451,11 @@ struct UnrollBodies<D, D> {
 
 // MBW: 16-row m-blocks per wave (4: 64 rows, one image row block; 2: half of one,
 // so a block covers 128 rows and the grid needs half the split-K slices).
-template <int NB, int NP, int D, int OCC = 1, bool PRE = false, int MBW = 4>
+// HALF (with PRE): S and Q both as their leading bf16 piece alone, one product per
+// fragment pair (~2^-9 relative: the solver's first sweeps, residual > 1e-2) - half
+// the S bytes of the PRE mode (the h slots of the two-piece image) and half the Q
+// image pieces.
+template <int NB, int NP, int D, int OCC = 1, bool PRE = false, int MBW = 4, bool HALF = false>
 __global__ __launch_bounds__(256, OCC) void sweep3_kernel(const f32x4* __restrict__ SI, int64_t d,
                                                         const u32x4* __restrict__ QS,
                                                         int64_t ngrp, float* __restrict__ Y,
@@ -471,7 +475,10 @@ __global__ __launch_bounds__(256, OCC) void sweep3_kernel(const f32x4* __restric
   }
   constexpr int MB = MBW;
   static_assert(MB == 2 || MB == 4, "m-blocks per wave");
-  constexpr int U = NP * NB;         // 1-KiB Q pieces per k-group
+  static_assert(!HALF || PRE, "the one-piece mode reads the two-piece image");
+  constexpr int QU = NP * NB;        // 1-KiB Q image pieces per k-group
+  constexpr int U = HALF ? NB : QU;  // of those, staged (HALF: the h piece of each block)
+  constexpr int SPC = HALF ? 1 : 2;  // S image slots loaded per m-block
   constexpr int ND = (U + 3) / 4;    // DMAs per wave per group (tail pieces repeated)
   constexpr int SLOT = U * 1024;     // bytes per ring slot
   constexpr int NS = D + 1;          // ring slots
@@ -494,7 +501,7 @@ __global__ __launch_bounds__(256, OCC) void sweep3_kernel(const f32x4* __restric
     for (int j = 0; j < NB; ++j) acc[mb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<u32x4*>(QS), 0, (int)(ngrp * U * 1024), 0x00020000);
+      const_cast<u32x4*>(QS), 0, (int)(ngrp * QU * 1024), 0x00020000);
   // image row block row0 / 64, starting at its m-block (row0 % 64) / 16
   const f32x4* sw = SI + (row0 / SI_RB) * ngrp * (4 * 2 * 64) + ((row0 % SI_RB) / 16) * 2 * 64 + lane;
   f32x4 sr[D][MB][2];
@@ -505,26 +512,31 @@ __global__ __launch_bounds__(256, OCC) void sweep3_kernel(const f32x4* __restric
 #pragma unroll
     for (int i = 0; i < ND; ++i) {
       const int u = wave + 4 * i < U ? wave + 4 * i : U - 1;
-      sw_dma16(qrs, (int)((g * U + u) * 1024) + lane * 16, slot + u * 1024);
+      const int64_t src = HALF ? (g * NB + u) * NP : g * U + u;
+      sw_dma16(qrs, (int)(src * 1024) + lane * 16, slot + u * 1024);
     }
     const f32x4* sg = sw + g * (4 * 2 * 64);
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) sr[b][mb][h] = sg[(mb * 2 + h) * 64];
+      for (int h = 0; h < SPC; ++h) sr[b][mb][h] = sg[(mb * 2 + h) * 64];
   };
   auto body = [&](auto Bc, int64_t g) {
     constexpr int B = decltype(Bc)::value;
     // Everything issued before the D - 1 younger groups has landed: this
     // group's Q pieces (every wave's, after the barrier) and S registers.
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"((D - 1) * (ND + 2 * MB))
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"((D - 1) * (ND + SPC * MB))
                  : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     u32x4 ah[MB], am[MB], al[MB];
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
-      if constexpr (PRE) {
+      if constexpr (HALF) {
+        ah[mb] = __builtin_bit_cast(u32x4, sr[B][mb][0]);
+        am[mb] = ah[mb];
+        al[mb] = ah[mb];
+      } else if constexpr (PRE) {
         ah[mb] = __builtin_bit_cast(u32x4, sr[B][mb][0]);
         am[mb] = __builtin_bit_cast(u32x4, sr[B][mb][1]);
         al[mb] = am[mb];  // unused by the SP = 2 products
@@ -533,6 +545,14 @@ __global__ __launch_bounds__(256, OCC) void sweep3_kernel(const f32x4* __restric
       }
     }
     const u32x4* qs = reinterpret_cast<const u32x4*>(qlds + (int)(g % NS) * SLOT) + lane;
+    if constexpr (HALF) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const u32x4 bh = qs[j * 64];
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(ah[mb], bh, acc[mb][j]);
+      }
+    } else
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const u32x4 bh = qs[(j * NP + 0) * 64], bm = qs[(j * NP + 1) * 64];
@@ -767,16 +787,28 @@ void launch_v2(Grid g, hipStream_t st, const f32x4* SI, int64_t d, const u32x4* 
                      ldy, alpha, part, g.per, *g.sb);
 }
 
-template <int NB, int NP, bool PRE>
+template <int NB, int NP, bool PRE, bool HALF = false>
 void launch_v3(Grid g, hipStream_t st, const f32x4* SI, int64_t d, const u32x4* QS, float* Y,
                int64_t ldy, float alpha, float* part) {
   const int64_t ng = si_groups(d);
   if (sweep_mb(PRE, NB) == 2)
-    hipLaunchKernelGGL((sweep3_kernel<NB, NP, kSweepDepth, 1, PRE, 2>), g.dim(), dim3(256), 0, st,
+    hipLaunchKernelGGL((sweep3_kernel<NB, NP, kSweepDepth, 1, PRE, 2, HALF>), g.dim(), dim3(256), 0, st,
                        SI, d, QS, ng, Y, ldy, alpha, part, g.per, *g.sb);
   else
-    hipLaunchKernelGGL((sweep3_kernel<NB, NP, kSweepDepth, 1, PRE>), g.dim(), dim3(256), 0, st, SI,
-                       d, QS, ng, Y, ldy, alpha, part, g.per, *g.sb);
+    hipLaunchKernelGGL((sweep3_kernel<NB, NP, kSweepDepth, 1, PRE, 4, HALF>), g.dim(), dim3(256), 0, st,
+                       SI, d, QS, ng, Y, ldy, alpha, part, g.per, *g.sb);
+}
+
+// The one-piece mode (v3 only, p >= 64: nb 4 .. 8).
+void launch_half(int nb, Grid grid, hipStream_t st, const f32x4* SI, int64_t d, const u32x4* QS,
+                 float* Y, int64_t ldy, float alpha, float* part) {
+  switch (nb) {
+    case 4: launch_v3<4, 2, true, true>(grid, st, SI, d, QS, Y, ldy, alpha, part); return;
+    case 5: launch_v3<5, 2, true, true>(grid, st, SI, d, QS, Y, ldy, alpha, part); return;
+    case 6: launch_v3<6, 2, true, true>(grid, st, SI, d, QS, Y, ldy, alpha, part); return;
+    case 7: launch_v3<7, 2, true, true>(grid, st, SI, d, QS, Y, ldy, alpha, part); return;
+    default: launch_v3<8, 2, true, true>(grid, st, SI, d, QS, Y, ldy, alpha, part); return;
+  }
 }
 
 // v2 (sweep3 = false) or v3 with NP Q pieces, NB = p / 16 column blocks; PRE: the
@@ -875,7 +907,9 @@ int sweep_apply(const float* Q, int64_t d, int p, int64_t ldq, float* Y, int64_t
   const int nb = p / 16;
   const int64_t ngrp = 2 * cdiv(d, SW_KS);
   const int np = round_q ? kRoundPieces : 3;
-  const bool pre = mode == 2 && np == 2;
+  // kSweepHalf (3) where the v3 kernel runs (p >= 64), else the two-piece mode
+  const bool half = mode == kSweepHalf && nb >= 4;
+  const bool pre = (mode == kSweepFast || mode == kSweepHalf) && np == 2;
   const dim3 qgrid((unsigned)cdiv(ngrp * nb * 64, 256));
   // q_ready: the previous sweep's finish kernel already wrote this Q's image
   if (!q_ready) {
@@ -900,7 +934,9 @@ int sweep_apply(const float* Q, int64_t d, int p, int64_t ldq, float* Y, int64_t
   // c1g 14.9 vs 15.3 M samples/s, profiles/r04f_bench_*)
   const int ks = sweep_ks_mb(d, mbw);
   const Grid grid{(int)(bx * ks), sb};
-  if (pre)
+  if (half)
+    launch_half(nb, grid, st, reinterpret_cast<const f32x4*>(w.SH), d, w.QS, Y, ldy, alpha, w.part);
+  else if (pre)
     launch_image<2, true>(v3, nb, grid, st, reinterpret_cast<const f32x4*>(w.SH), d, w.QS, Y, ldy,
                           alpha, w.part);
   else if (np == 2)

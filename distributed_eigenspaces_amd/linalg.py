@@ -581,7 +581,7 @@ def oja_steps(X: torch.Tensor, V: torch.Tensor, eta: float, batch: int,
 # ---------------------------------------------------------------- sweep
 def sym_apply(S: torch.Tensor, Q: torch.Tensor, algo: str = "auto", alpha: float = 1.0,
               out: torch.Tensor | None = None, prepared: bool = False,
-              round_q: bool = False, fast: bool = False,
+              round_q: bool = False, fast: bool = False, half: bool = False,
               kernel_only: bool = False) -> torch.Tensor:
     """Y = alpha * S Q for symmetric S (d x d) and Q (d x p, p % 16 == 0, p <= 128):
     one subspace-iteration sweep of ``topk_eigh`` (include/deig.h DEIG_SWEEP_*):
@@ -592,9 +592,12 @@ def sym_apply(S: torch.Tensor, Q: torch.Tensor, algo: str = "auto", alpha: float
     modified in place) is rounded to its two leading bf16 pieces and Y = alpha S Q'
     is formed from five bf16 products.  ``fast=True`` (implies round_q; the solver's
     early-sweep mode, DEIG_SWEEP_FAST): S is also taken as its two leading bf16
-    pieces, three products, ~2^-16 relative.  ``kernel_only=True`` (measurement,
+    pieces, three products, ~2^-16 relative.  ``half=True`` (implies fast; the
+    solver's first sweeps, DEIG_SWEEP_HALF, p >= 64): S and Q as their leading bf16
+    piece alone, one product, ~2^-9 relative.  ``kernel_only=True`` (measurement,
     DEIG_SWEEP_KERNEL_ONLY): only the sweep kernel runs, on the Q image the previous
     call in this stream's workspace left; ``out`` is not written."""
+    fast = fast or half
     round_q = round_q or fast
     if algo not in _lib.SWEEP_ALGOS:
         raise ValueError(f"algo must be one of {sorted(_lib.SWEEP_ALGOS)}, got {algo!r}")
@@ -619,6 +622,8 @@ def sym_apply(S: torch.Tensor, Q: torch.Tensor, algo: str = "auto", alpha: float
         code |= _lib.DEIG_SWEEP_ROUND_Q
     if fast:
         code |= _lib.DEIG_SWEEP_FAST
+    if half:
+        code |= _lib.DEIG_SWEEP_HALF
     if kernel_only:
         if code & 0xff == _lib.DEIG_SWEEP_FP32:
             raise ValueError("kernel_only needs algo bf16x6/auto")
@@ -636,13 +641,14 @@ def sym_apply(S: torch.Tensor, Q: torch.Tensor, algo: str = "auto", alpha: float
 
 def sym_power(S: torch.Tensor, Q: torch.Tensor, cs: torch.Tensor, steps: int,
               out: torch.Tensor | None = None, prepared: bool = False,
-              round_q: bool = False, fast: bool = False) -> torch.Tensor:
+              round_q: bool = False, fast: bool = False, half: bool = False) -> torch.Tensor:
     """``steps`` sweeps of the solver's power chain (include/deig.h
     deig_sym_power_f32): Y = S Q, then Q_j <- cs_j Y_j on the columns with
     cs_j > 0, each step fused into the sweep's split-K reduction with the next
     sweep's Q image, as between the Rayleigh-Ritz steps of ``topk_eigh``.  Q
     (contiguous float32, d x p) is updated in place; returns Y = S Q_{steps-1}.
     Flags as for ``sym_apply`` (bf16x6 only)."""
+    fast = fast or half
     round_q = round_q or fast
     S = require_device_tensor(S, "sym_power")
     Q = require_device_tensor(Q, "Q")
@@ -665,6 +671,8 @@ def sym_power(S: torch.Tensor, Q: torch.Tensor, cs: torch.Tensor, steps: int,
         code |= _lib.DEIG_SWEEP_ROUND_Q
     if fast:
         code |= _lib.DEIG_SWEEP_FAST
+    if half:
+        code |= _lib.DEIG_SWEEP_HALF
     L = _lib.lib()
     with torch.cuda.device(S.device):
         nbytes = L.deig_sym_apply_workspace(d, p, code)

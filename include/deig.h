@@ -159,8 +159,16 @@ int deig_default_subspace(int64_t d, int k);
  * (from a two-piece image written by the same prepare pass), so Y = alpha S' Q' is
  * three bf16 MFMA products (hh + hm + mh) with no split in the sweep: ~2^-16
  * relative (S' rounding 2^-17, dropped m m 2^-18).  deig_topk_sym_f32 uses it while
- * its residual is above 1e-3, ROUND_Q down to 1e-4, the exact product below. */
+ * its residual is above 1e-3 (after the one-product HALF sweeps above 1e-2), ROUND_Q
+ * down to 1e-4, the exact product below. */
 #define DEIG_SWEEP_FAST 0x400
+/* OR-ed into the algorithm of deig_sym_apply_f32 / deig_sym_power_f32 (BF16X6 only;
+ * implies FAST): the solver's first sweeps.  S and Q are both taken as their leading
+ * bf16 piece alone (the h slots of the two-piece image: half its bytes), one bf16
+ * MFMA product per fragment pair, ~2^-9 relative.  Needs p >= 64 (below, the FAST
+ * mode runs).  deig_topk_sym_f32 uses it while its residual is above
+ * deig_solver_opts.half_until (1e-2). */
+#define DEIG_SWEEP_HALF 0x1000
 /* OR-ed into the algorithm of deig_sym_apply_f32 (BF16X6 only; measurement):
  * launch the sweep kernel alone on the Q image that the previous call with the
  * same workspace, d, p and mode left - no split of Q, no split-K reduction, Y is
@@ -211,6 +219,8 @@ typedef struct deig_solver_opts {
   float fast_until;          /* three-product sweeps while resid > this (1e-3; 0: never) */
   float round_until;         /* five-product sweeps while resid > this (1e-4) */
   int debug;                 /* 1: per-Rayleigh-Ritz trace on stderr */
+  float half_until;          /* one-product sweeps (DEIG_SWEEP_HALF) while resid > this
+                                (1e-2; 0: never) */
 } deig_solver_opts;
 void deig_solver_opts_init(deig_solver_opts* opts);
 

@@ -109,6 +109,7 @@ def test_solver_opts_struct_and_defaults():
     assert (o.chebyshev, o.deflate, o.deflate_early, o.rr_every) == (1, 1, 1, 0)
     assert o.cheb_above < 0 and abs(o.fast_until - 1e-3) < 1e-9  # cheb_above: per solve
     assert abs(o.round_until - 1e-4) < 1e-9 and o.jacobi_early_sweeps == -1
+    assert abs(o.half_until - 1e-2) < 1e-9
     bad = _lib.SolverOpts()
     bad.size = 4
     V = ctypes.c_int(0)

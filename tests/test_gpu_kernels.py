@@ -274,6 +274,56 @@ def test_sym_apply_fast(d, p, cuda):
     assert np.abs(Y6 - ref).max() / np.abs(ref).max() <= 2e-6
 
 
+@pytest.mark.parametrize("d,p", [(520, 80), (300, 128), (8192, 80), (4100, 96), (2048, 64), (16384, 128)])
+def test_sym_apply_half(d, p, cuda):
+    """The solver's first sweeps (DEIG_SWEEP_HALF, p >= 64): Q rounded in place as in
+    round_q, then S and Q both taken as their leading bf16 piece (round to nearest
+    even), one product.  Against float64 bf16(S) @ bf16(Q) only the fp32
+    accumulation differs; against the exact S @ Q' it is ~2^-9 relative."""
+    import distributed_eigenspaces_amd as de
+    rng = np.random.default_rng(13 * d + p)
+    A = rng.standard_normal((d, d)).astype(np.float32)
+    S = ((A + A.T) * 0.5).astype(np.float32)
+    Q = rng.standard_normal((d, p)).astype(np.float32)
+    St = torch.from_numpy(S).to(cuda)
+    Qt = torch.from_numpy(Q).to(cuda)
+    Sh = torch.from_numpy(S).to(torch.bfloat16).double().numpy()
+    for it in range(2):
+        Y = de.sym_apply(St, Qt, prepared=it > 0, half=True).cpu().numpy().astype(np.float64)
+        Qr = Qt.cpu().numpy()
+        assert np.all(np.abs(Qr - Q) <= 2.0 ** -17 * np.abs(Q) * 1.0001), "rounding exceeds 2^-17"
+        # the h piece of the Q the call received (bf16(Q') can differ from it where m
+        # is exactly half an ulp of h: a tie)
+        Qh = torch.from_numpy(Q).to(torch.bfloat16).double().numpy()
+        ref1 = Sh @ Qh
+        ref = S.astype(np.float64) @ Qr.astype(np.float64)
+        scale = np.abs(ref).max()
+        assert np.abs(Y - ref1).max() / scale <= 1e-5, f"half sweep vs h(S)h(Q) d={d} p={p} it={it}"
+        assert np.abs(Y - ref).max() / scale <= 1e-2, f"half sweep vs SQ' d={d} p={p} it={it}"
+        Q = Qr
+    # the other modes still read their own paths after a half call on one image
+    Y3 = de.sym_apply(St, Qt, prepared=True, fast=True).cpu().numpy()
+    Y6 = de.sym_apply(St, Qt, prepared=True).cpu().numpy()
+    ref = S.astype(np.float64) @ Qt.cpu().numpy().astype(np.float64)
+    assert np.abs(Y3 - ref).max() / np.abs(ref).max() <= 6e-5
+    assert np.abs(Y6 - ref).max() / np.abs(ref).max() <= 2e-6
+
+
+@pytest.mark.parametrize("d,p", [(1000, 16), (3072, 48)])
+def test_sym_apply_half_below_p64_is_fast(d, p, cuda):
+    """Below p = 64 (no v3 sweep kernel) DEIG_SWEEP_HALF runs the FAST mode: the same
+    bits as fast=True on the same input."""
+    import distributed_eigenspaces_amd as de
+    rng = np.random.default_rng(d * p)
+    A = rng.standard_normal((d, d)).astype(np.float32)
+    St = torch.from_numpy((A + A.T) * 0.5).to(cuda)
+    Q = torch.from_numpy(rng.standard_normal((d, p)).astype(np.float32)).to(cuda)
+    Q2 = Q.clone()
+    Yh = de.sym_apply(St, Q, half=True)
+    Yf = de.sym_apply(St, Q2, fast=True)
+    assert torch.equal(Yh, Yf) and torch.equal(Q, Q2)
+
+
 def test_sym_apply_rejects_bad_p(cuda):
     import distributed_eigenspaces_amd as de
     S = torch.eye(64, device=cuda)
@@ -283,7 +333,8 @@ def test_sym_apply_rejects_bad_p(cuda):
 
 
 @pytest.mark.parametrize("d,p,mode", [(512, 32, "exact"), (1000, 48, "round_q"), (3072, 32, "fast"),
-                                      (8192, 80, "fast"), (2048, 128, "exact")])
+                                      (8192, 80, "fast"), (2048, 128, "exact"), (8192, 80, "half"),
+                                      (4096, 128, "half")])
 def test_sym_power_fused_chain(d, p, mode, cuda):
     """The solver's sweep chain with the power step, the split-K reduction and the
     next sweep's Q image fused (sweep_finish_kernel) vs the same chain in float64:
@@ -298,7 +349,7 @@ def test_sym_power_fused_chain(d, p, mode, cuda):
     steps = 4
     St = torch.from_numpy(S).to(cuda)
     Q = torch.from_numpy(Q0).to(cuda)
-    kw = {"round_q": mode == "round_q", "fast": mode == "fast"}
+    kw = {"round_q": mode == "round_q", "fast": mode == "fast", "half": mode == "half"}
     Y = de.sym_power(St, Q, torch.from_numpy(cs), steps, **kw)
     Qr, S64 = Q0.astype(np.float64), S.astype(np.float64)
     for _ in range(steps):
@@ -306,7 +357,7 @@ def test_sym_power_fused_chain(d, p, mode, cuda):
         Qn = Yr * cs
         Qn[:, cs <= 0] = Qr[:, cs <= 0]
         Qr = Qn
-    tol = {"exact": 6e-6, "round_q": 5e-5, "fast": 2e-4}[mode]
+    tol = {"exact": 6e-6, "round_q": 5e-5, "fast": 2e-4, "half": 2e-2}[mode]
     for got, ref in ((Y.cpu().numpy(), Yr), (Q.cpu().numpy(), Qr)):
         err = np.abs(got - ref).max() / np.abs(ref).max()
         assert err <= tol, f"sym_power[{mode}] d={d} p={p}: rel err {err:.3e} > {tol:.1e}"
