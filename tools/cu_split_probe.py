@@ -10,7 +10,7 @@ workers' covariances on a disjoint set of CUs?
 
   python tools/cu_split_probe.py probe
   DEIG_LIB_PATH=tools/ab_libs/libdeig_syrk_g232.so python tools/cu_split_probe.py pipe --solve-cus 24
-  python tools/cu_split_probe.py serial
+  python tools/cu_split_probe.py serial [--case c5|c3] [--half-until 0]
 """
 import argparse
 import ctypes
@@ -90,6 +90,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--workers", type=int, default=8)
     ap.add_argument("--case", default="c5")
+    ap.add_argument("--half-until", type=float, default=None,
+                    help="serial: deig_solver_opts.half_until (default: the library's)")
     a = ap.parse_args()
     import torch
     torch.cuda.init()
@@ -121,11 +123,14 @@ def main():
     res = {"mode": a.mode, "case": a.case, "lib": os.environ.get("DEIG_LIB_PATH", "shipped")}
     if a.mode == "serial":
         st = torch.cuda.current_stream(dev)
+        from distributed_eigenspaces_amd import _lib
+        opts = _lib.solver_opts(half_until=a.half_until)
+        res["half_until"] = float(opts.half_until)
 
         def step():
             for w in range(W):
                 de.sigma_hat(X[w * n:(w + 1) * n], out=Ss[w])
-            rs = de.topk_eigh_batch(Ss, k, check_finite=False)
+            rs = de.topk_eigh_batch(Ss, k, check_finite=False, opts=opts)
             for w, r in enumerate(rs):
                 Wt[w * k:(w + 1) * k].copy_(r.V.t())
             torch.cuda.synchronize()
