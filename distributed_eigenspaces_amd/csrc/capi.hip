@@ -407,6 +407,8 @@ StatusPool& status_pool() {
   return pool;
 }
 
+constexpr int64_t kHalfMinD = 2048;  // smallest d for the one-product early sweeps
+
 struct Solver {
   Operator op;
   Opts o;
@@ -544,7 +546,13 @@ struct Solver {
     // then Q rounded to two pieces (five products) down to round_until; the
     // closing sweeps exact (the rounding puts ~4e-6 relative noise into the basis
     // each sweep: a floor under the residual).
-    const int smode = (o.half_until > 0.f && last > fmaxf(o.half_until, tol))     ? kSweepHalf
+    // One-product sweeps (~2^-9) while the residual is above half_until, from
+    // d = 2048 on: there the sweep streams S from HBM and the mode halves its bytes
+    // (c5 worker solve 8.3 -> 6.9 ms); below it the sweep is latency-bound, and two
+    // small-d edge cases (k = 97 of d = 100, k = 200 rank-deficient at d = 512) lost
+    // convergence with it.
+    const bool half_ok = o.half_until > 0.f && d >= kHalfMinD;
+    const int smode = (half_ok && last > fmaxf(o.half_until, tol))                ? kSweepHalf
                       : (o.fast_until > 0.f && last > fmaxf(o.fast_until, tol)) ? kSweepFast
                       : last > fmaxf(o.round_until, tol)                      ? kSweepRoundQ
                                                                               : kSweepExact;

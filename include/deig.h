@@ -219,8 +219,8 @@ typedef struct deig_solver_opts {
   float fast_until;          /* three-product sweeps while resid > this (1e-3; 0: never) */
   float round_until;         /* five-product sweeps while resid > this (1e-4) */
   int debug;                 /* 1: per-Rayleigh-Ritz trace on stderr */
-  float half_until;          /* one-product sweeps (DEIG_SWEEP_HALF) while resid > this
-                                (1e-2; 0: never) */
+  float half_until;          /* one-product sweeps (DEIG_SWEEP_HALF) while resid > this,
+                                for d >= 2048 and p >= 64 (1e-2; 0: never) */
 } deig_solver_opts;
 void deig_solver_opts_init(deig_solver_opts* opts);
 

@@ -165,3 +165,58 @@ def test_k_outside_range_is_a_clear_error(cuda):
         de.topk_eigh(S, 257)
     with pytest.raises(ValueError, match="out of range"):
         de.topk_eigh(S, 0)
+
+
+def _solve_both(S, k, **kw):
+    """The solve with the default one-product early sweeps (d >= 2048) and without
+    them (deig_solver_opts.half_until = 0); neither may warn NotConverged."""
+    import distributed_eigenspaces_amd as de
+    from distributed_eigenspaces_amd import _lib
+    out = []
+    for h in (None, 0.0):
+        with warnings.catch_warnings():
+            warnings.simplefilter("error")
+            out.append(de.topk_eigh(S, k, opts=_lib.solver_opts(half_until=h), **kw))
+    return out
+
+
+@pytest.mark.parametrize("d,n,k", [(2048, 150, 200), (4096, 1500, 64)])
+def test_half_sweeps_rank_deficient_large_d(d, n, k, cuda):
+    """The one-product early sweeps (2^-9 products while the residual is above 1e-2)
+    on rank-deficient covariances at the widths that use them, one with k > 128
+    (block locking over S's null space): the same converged answer as without them
+    - top-rank subspace and eigenvalues against float64 eigh, null pairs ~0."""
+    g = torch.Generator(device="cpu").manual_seed(d + n)
+    X = torch.randn(n, d, generator=g, dtype=torch.float64)
+    X *= torch.linspace(3.0, 1.0, d, dtype=torch.float64)
+    S64 = (X.t() @ X / n).numpy()
+    S = torch.from_numpy(S64.astype(np.float32)).to(cuda)
+    w, V = np.linalg.eigh(S.double().cpu().numpy())
+    top = min(k, n)
+    for r in _solve_both(S, k):
+        assert r.converged
+        Vg = r.V.double().cpu().numpy()
+        assert np.abs(Vg.T @ Vg - np.eye(k)).max() < 1e-4
+        ev = r.evals.double().cpu().numpy()
+        np.testing.assert_allclose(ev[k - top:], w[-top:], rtol=EV_TOL)
+        Vt, Vr = Vg[:, k - top:], V[:, -top:]
+        assert np.linalg.norm(Vt @ Vt.T - Vr @ Vr.T) <= 10 * P_TOL * np.sqrt(top)
+        if k > n:
+            assert np.abs(ev[:k - top]).max() <= 1e-5 * w[-1]
+
+
+@pytest.mark.parametrize("ratio", [0.9, 0.95])
+def test_half_sweeps_small_gap_large_d(ratio, cuda):
+    """A small eigengap at k (lambda_{k+1}/lambda_k = ratio) at d = 2048, k = 64: with
+    and without the one-product early sweeps the solve converges to the same basis."""
+    d, k = 2048, 64
+    S = torch.from_numpy(_matrix(_flat_tail(d, k, ratio), seed=int(ratio * 100))).to(cuda)
+    a, b = _solve_both(S, k, max_sweeps=600)
+    w, V = np.linalg.eigh(S.double().cpu().numpy())
+    for r in (a, b):
+        assert r.converged
+        Vg = r.V.double().cpu().numpy()
+        dist = np.linalg.norm(Vg @ Vg.T - V[:, -k:] @ V[:, -k:].T)
+        assert dist <= P_TOL, f"ratio {ratio}: {dist:.2e}"
+        np.testing.assert_allclose(r.evals.double().cpu().numpy(), w[-k:], rtol=EV_TOL)
+    assert a.sweeps <= 1.5 * b.sweeps + 10, (a.sweeps, b.sweeps)
