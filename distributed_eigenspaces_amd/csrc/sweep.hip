@@ -756,6 +756,11 @@ constexpr int kSweepDepth = DEIG_AB_SWEEP_DEPTH;
 #else
 constexpr int kSweepDepth = 3;
 #endif
+#ifdef DEIG_AB_SWEEP_HALF_DEPTH
+constexpr int kSweepDepthHalf = DEIG_AB_SWEEP_HALF_DEPTH;
+#else
+constexpr int kSweepDepthHalf = 3;
+#endif
 
 // Split-K slices of a v3 launch with mb m-blocks per wave (rows per block 64 mb).
 int sweep_ks_mb(int64_t d, int mb) {
@@ -791,11 +796,12 @@ template <int NB, int NP, bool PRE, bool HALF = false>
 void launch_v3(Grid g, hipStream_t st, const f32x4* SI, int64_t d, const u32x4* QS, float* Y,
                int64_t ldy, float alpha, float* part) {
   const int64_t ng = si_groups(d);
+  constexpr int D = HALF ? kSweepDepthHalf : kSweepDepth;
   if (sweep_mb(PRE, NB) == 2)
-    hipLaunchKernelGGL((sweep3_kernel<NB, NP, kSweepDepth, 1, PRE, 2, HALF>), g.dim(), dim3(256), 0, st,
+    hipLaunchKernelGGL((sweep3_kernel<NB, NP, D, 1, PRE, 2, HALF>), g.dim(), dim3(256), 0, st,
                        SI, d, QS, ng, Y, ldy, alpha, part, g.per, *g.sb);
   else
-    hipLaunchKernelGGL((sweep3_kernel<NB, NP, kSweepDepth, 1, PRE, 4, HALF>), g.dim(), dim3(256), 0, st,
+    hipLaunchKernelGGL((sweep3_kernel<NB, NP, D, 1, PRE, 4, HALF>), g.dim(), dim3(256), 0, st,
                        SI, d, QS, ng, Y, ldy, alpha, part, g.per, *g.sb);
 }
 

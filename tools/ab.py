@@ -10,7 +10,7 @@ in-tree distributed_eigenspaces_amd/libdeig.so.
   python tools/ab.py build "MACRO=V [-DOTHER=W]" tools/ab_libs/libdeig_x.so   # here (CPU)
   python tools/ab.py syrk  REPS N D LIB [LIB ...]          # split3 covariance, ms per op
   python tools/ab.py sweep REPS D P MODE LIB [LIB ...]     # solver sweep chain, us per sweep
-                                                           # MODE bf16x3 | bf16x5 | bf16x6
+                                                           # MODE half | bf16x3 | bf16x5 | bf16x6
   python tools/ab.py oja   REPS ORTH LIB [LIB ...]         # config-4 Oja, us per batch
   python tools/ab.py rr    [LIB ...]                       # RR small-solve phases (DEIG_DEBUG)
   python tools/ab.py tests TAG LIB [LIB ...] [-- PYTEST ARGS]   # GPU suite per build
@@ -139,8 +139,10 @@ def ab_sweep(reps, d, p, mode, paths):
     code = _lib.DEIG_SWEEP_BF16X6
     if mode != "bf16x6":
         code |= _lib.DEIG_SWEEP_ROUND_Q
-    if mode == "bf16x3":
+    if mode in ("bf16x3", "half"):
         code |= _lib.DEIG_SWEEP_FAST
+    if mode == "half":
+        code |= _lib.DEIG_SWEEP_HALF
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev)
     g = torch.Generator(device=dev).manual_seed(5)
