@@ -1161,35 +1161,45 @@ int solve_batch(int W, const Operator* ops, int64_t d, int k, int p, int max_swe
   // workgroup per problem) or the host works through its status, the other group's
   // sweeps fill the GPU.  Every problem's launches are the same as in one group, so the
   // results are too (bit for bit).
-#ifndef DEIG_AB_BATCH_ONE_GROUP
   // (d >= 2048: below that the per-launch cost outweighs the overlap - config-1 gray
   // shards, d = 1024, measured 8 % slower with two groups)
-  const int NG = (W >= 2 && d >= 2048) ? 2 : 1;
+#if defined(DEIG_AB_BATCH_ONE_GROUP)
+  constexpr int kGroups = 1;
+#elif defined(DEIG_AB_BATCH_GROUPS)
+  constexpr int kGroups = DEIG_AB_BATCH_GROUPS;
 #else
-  const int NG = 1;
+  constexpr int kGroups = 2;
 #endif
-  hipStream_t gs[2] = {st, nullptr};
+  constexpr int kMaxGroups = 4;
+  static_assert(kGroups >= 1 && kGroups <= kMaxGroups, "stream groups");
+  const int NG = d >= 2048 ? std::min(kGroups, W) : 1;
+  hipStream_t gs[kMaxGroups] = {st, nullptr, nullptr, nullptr};
   hipEvent_t ev = nullptr;
   struct Cleanup {
-    hipStream_t& s2;
+    hipStream_t* s;
     hipEvent_t& e;
     ~Cleanup() {
       if (e) (void)hipEventDestroy(e);
-      if (s2) (void)hipStreamDestroy(s2);
+      for (int g = 1; g < kMaxGroups; ++g)
+        if (s[g]) (void)hipStreamDestroy(s[g]);
     }
-  } cleanup{gs[1], ev};
-  if (NG == 2) {
-    DEIG_HIP_CHECK(hipStreamCreateWithFlags(&gs[1], hipStreamNonBlocking));
+  } cleanup{gs, ev};
+  if (NG > 1) {
     DEIG_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     DEIG_HIP_CHECK(hipEventRecord(ev, st));  // the operators were written on st
-    DEIG_HIP_CHECK(hipStreamWaitEvent(gs[1], ev, 0));
+    for (int g = 1; g < NG; ++g) {
+      DEIG_HIP_CHECK(hipStreamCreateWithFlags(&gs[g], hipStreamNonBlocking));
+      DEIG_HIP_CHECK(hipStreamWaitEvent(gs[g], ev, 0));
+    }
   }
-  // the caller's stream waits for the second group's launches (before any return)
+  // the caller's stream waits for the other groups' launches (before any return)
   auto join = [&]() -> int {
-    if (NG == 1) return DEIG_OK;
-    const hipError_t e1 = hipEventRecord(ev, gs[1]);
-    const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(st, ev, 0) : e1;
-    return e2 == hipSuccess ? DEIG_OK : fail(DEIG_EHIP, "solve_batch: joining the second stream failed");
+    for (int g = 1; g < NG; ++g) {
+      const hipError_t e1 = hipEventRecord(ev, gs[g]);
+      const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(st, ev, 0) : e1;
+      if (e2 != hipSuccess) return fail(DEIG_EHIP, "solve_batch: joining a group's stream failed");
+    }
+    return DEIG_OK;
   };
   std::vector<SolveSM> sm(W);
   int rc = DEIG_OK;
@@ -1229,7 +1239,7 @@ int solve_batch(int W, const Operator* ops, int64_t d, int k, int p, int max_swe
   std::vector<int> jc;
   // one round's cycles of the problems in cyc, on stream st (stream-ordered after every
   // problem's set-up launches)
-  std::vector<int> cyc_g[2];
+  std::vector<int> cyc_g[kMaxGroups];
   auto run_round = [&](const std::vector<int>& cyc, hipStream_t st) -> int {
     size_t L = 0;
     for (int i : cyc) L = std::max(L, sm[i].sv.plan.size());
@@ -1336,7 +1346,12 @@ int solve_batch(int W, const Operator* ops, int64_t d, int k, int p, int max_swe
     return run_round(cy, gs[g]);
   };
   for (int g = 0; g < NG && !rc; ++g) rc = advance(g);
-  while (!rc && (!cyc_g[0].empty() || !cyc_g[1].empty())) {
+  auto pending = [&]() {
+    for (int g = 0; g < NG; ++g)
+      if (!cyc_g[g].empty()) return true;
+    return false;
+  };
+  while (!rc && pending()) {
     for (int g = 0; g < NG && !rc; ++g) {
       if (cyc_g[g].empty()) continue;
       if (hipStreamSynchronize(gs[g]) != hipSuccess) {
