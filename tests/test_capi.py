@@ -101,6 +101,20 @@ def test_workspace_fused_split_variant():
     assert L.deig_syrk_workspace_ex(1 << 21, 8192, _lib.DEIG_SYRK_SPLIT3) >= (1 << 21) * 8192 * 4
 
 
+def test_solver_opts_mirror_matches_header():
+    """The ctypes mirror lists deig_solver_opts' fields in the header's order with the
+    header's C types (a field added on one side only shifts every later one)."""
+    import os
+    import re
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "include", "deig.h")).read()
+    body = re.search(r"typedef struct deig_solver_opts \{(.*?)\} deig_solver_opts;", hdr, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    fields = re.findall(r"\b(int|float)\s+(\w+)\s*;", body)
+    ctype = {"int": ctypes.c_int, "float": ctypes.c_float}
+    assert [(n, ctype[t]) for t, n in fields] == list(_lib.SolverOpts._fields_)
+
+
 def test_solver_opts_struct_and_defaults():
     """deig_solver_opts: the ctypes mirror has the C size (the library checks it) and
     the defaults the r02 environment knobs had."""
