@@ -92,6 +92,8 @@ def main():
     ap.add_argument("--case", default="c5")
     ap.add_argument("--half-until", type=float, default=None,
                     help="serial: deig_solver_opts.half_until (default: the library's)")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="serial: another deig_solver_opts field, NAME=VALUE (repeatable)")
     a = ap.parse_args()
     import torch
     torch.cuda.init()
@@ -124,8 +126,10 @@ def main():
     if a.mode == "serial":
         st = torch.cuda.current_stream(dev)
         from distributed_eigenspaces_amd import _lib
-        opts = _lib.solver_opts(half_until=a.half_until)
+        extra = {kv.split("=")[0]: float(kv.split("=")[1]) for kv in a.opt}
+        opts = _lib.solver_opts(half_until=a.half_until, **extra)
         res["half_until"] = float(opts.half_until)
+        res["opts"] = extra
 
         def step():
             for w in range(W):
