@@ -11,6 +11,7 @@ workers' covariances on a disjoint set of CUs?
   python tools/cu_split_probe.py probe
   DEIG_LIB_PATH=tools/ab_libs/libdeig_syrk_g232.so python tools/cu_split_probe.py pipe --solve-cus 24
   python tools/cu_split_probe.py serial [--case c5|c3] [--half-until 0]
+  python tools/cu_split_probe.py solve [--case c5|c3]     (the batched solves alone)
 """
 import argparse
 import ctypes
@@ -85,7 +86,7 @@ def decide(P, torch):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["probe", "pipe", "serial"])
+    ap.add_argument("mode", choices=["probe", "pipe", "serial", "solve"])
     ap.add_argument("--solve-cus", type=int, default=24)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--workers", type=int, default=8)
@@ -123,6 +124,20 @@ def main():
         return float((1 - sv.min() ** 2).clamp(min=0).sqrt())
 
     res = {"mode": a.mode, "case": a.case, "lib": os.environ.get("DEIG_LIB_PATH", "shipped")}
+    if a.mode == "solve":  # the batched worker solves alone (covariances once, untimed)
+        for w in range(W):
+            de.sigma_hat(X[w * n:(w + 1) * n], out=Ss[w])
+        del X
+        ts = []
+        for _ in range(a.reps + 1):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            rs = de.topk_eigh_batch(Ss, k, check_finite=False)
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        res.update(solve_ms=[round(t, 3) for t in ts[1:]], sweeps=[r.sweeps for r in rs])
+        print(json.dumps(res), flush=True)
+        return
     if a.mode == "serial":
         st = torch.cuda.current_stream(dev)
         from distributed_eigenspaces_amd import _lib
