@@ -1760,7 +1760,11 @@ size_t rr_small_shm(int p) {
   return (size_t)(2 * p * p + 7 * p + RT / 64 + 20) * sizeof(float);
 }
 
+#ifdef DEIG_AB_RR_THREADS
+constexpr int RT2 = DEIG_AB_RR_THREADS;  // measurement builds
+#else
 constexpr int RT2 = 1024;  // rr_small2 (the Jacobi's per-step work wants every thread)
+#endif
 size_t rr_small2_shm(int p) {
   return (size_t)(2 * p * p + 9 * p + 16 * 17 + 4 + 16 * (p + 4) + RT2 / 64 + 2 + 4) * sizeof(float);
 }
